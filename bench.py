@@ -1,0 +1,262 @@
+#!/usr/bin/env python
+"""Benchmark: audio-codes/s + RTF of the tts.inference hot path on MI355X.
+
+One "step" = one pass of the hot path over one batch of synthetic utterances per GPU:
+greedy SpeechLM generation of N codes after a P-token prompt (prefill + N decode steps,
+`max_length = P + N`, `min_new_tokens = N`, repetition penalty 1.1: the semantics of
+tts/inference/inferencing.py:94-107) followed by the codec decode of each utterance's
+prompt + generated codes at 24 kHz (decoding.py:84-89).  Timing boundary = the reference's
+(generate + codec decode, inferencing.py:153-155,209-220).
+
+Default workload (BASELINE.json configs[1]): TTS-1 bf16 (Llama-3.2-1B dims, V=193,856),
+batch 1 per GPU, P = 200 (150 prompt codes), N = 500 codes (10 s of audio), codec 24 kHz
+(hop 160, ups [3]) on 650 codes.  Random-init weights of that architecture (no checkpoint
+is reachable offline); synthetic token ids of the reference prompt shape.
+
+Multi-GPU (torchrun): one process per GPU.  Rank 0 builds the request batch and
+broadcasts it over RCCL; each rank decodes its contiguous shard; generated codes are
+gathered back to rank 0 (the only exchange steps of the path).  Weak scaling.
+
+Prints ONE JSON line (rank 0).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tts-max_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU per step")
+    ap.add_argument("--arch", default="tts1")
+    ap.add_argument("--codec", default="codec-24k")
+    ap.add_argument("--prompt-codes", type=int, default=150)
+    ap.add_argument("--text-tokens", type=int, default=39)
+    ap.add_argument("--new", type=int, default=500)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--kernel-iters", type=int, default=30)
+    args = ap.parse_args()
+
+    from tts_amd import configs, synth
+    from tts_amd.codec import MI355XAudioDecoder
+    from tts_amd.speechlm import MI355XSpeechLM
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    arch = configs.LM_ARCHS[args.arch]
+    carch = configs.CODEC_ARCHS[args.codec]
+    vocab = configs.vocab_for(arch)
+    B = args.batch
+    N = args.new
+
+    # ---- requests: rank 0 builds all world*B prompts, broadcast over RCCL
+    prompts_all = [synth.synthetic_prompt(vocab, u, args.text_tokens, args.prompt_codes) for u in range(world * B)]
+    P = max(len(p) for p in prompts_all)
+    req = torch.zeros(world * B, P + 1, dtype=torch.int32, device=dev)
+    if rank == 0:
+        for i, p in enumerate(prompts_all):
+            req[i, 0] = len(p)
+            req[i, 1:1 + len(p)] = torch.tensor(p, dtype=torch.int32)
+
+    max_seq = P + N + 16
+    t0 = time.time()
+    lm = MI355XSpeechLM.synthetic(arch, seed=0x5EED, device=local, max_batch=B, max_seq_len=max_seq)
+    dec = MI355XAudioDecoder.synthetic(carch, seed=0xC0DEC, device=local, max_codes=args.prompt_codes + N + 8)
+    log(f"[rank {rank}] engine ready in {time.time() - t0:.1f}s")
+    codes_per_utt = args.prompt_codes + N
+
+    def one_step():
+        if dist is not None:
+            dist.broadcast(req, src=0)
+        mine = req[rank * B:(rank + 1) * B].cpu()
+        prompts = [mine[i, 1:1 + int(mine[i, 0])].tolist() for i in range(B)]
+        new = lm.generate_batch(prompts, max_length=P + N, min_new_tokens=N, eos_token_id=vocab.speech_end_id,
+                                repetition_penalty=1.1)
+        # codec input = prompt speech codes + generated codes (ids -> codes via the LUT)
+        utts = []
+        for p, n in zip(prompts, new):
+            codes = [c for c in lm.ids_to_codes(p[-args.prompt_codes:] + n) if c >= 0]
+            utts.append(codes)
+        wav = dec.decode_batch(utts, out=wav_buf)
+        out = torch.full((B, N), -1, dtype=torch.int32, device=dev)
+        for i, n in enumerate(new):
+            out[i, :len(n)] = torch.tensor(n, dtype=torch.int32)
+        if dist is not None:
+            gathered = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
+            dist.gather(out, gathered, dst=0)
+        return sum(len(n) for n in new), wav
+
+    wav_buf = torch.empty(B * codes_per_utt * carch.samples_per_code, dtype=torch.float32, device=dev)
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    n_codes = 0
+    lm_prefill = lm_decode = 0.0
+    dec_steps = 0
+    for _ in range(args.steps):
+        n, _ = one_step()
+        n_codes += n
+        a, b, k = lm.last_timing()
+        lm_prefill += a
+        lm_decode += b
+        dec_steps += k
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot = torch.tensor([n_codes], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_codes = float(tot.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    codes_per_s = total_codes / elapsed
+    audio_s = N / carch.token_rate  # seconds of audio per utterance
+    rtf = (elapsed / args.steps) / audio_s  # wall per utterance-batch / audio seconds (per GPU)
+
+    # ---- roofline of the dominant kernel (and the whole decode step), live HIP events
+    kern = {}
+    ctx_mid = P + N // 2
+    for k in lm.KERNELS:
+        ms, by = lm.bench_kernel(k, rows=B, ctx=ctx_mid, iters=args.kernel_iters)
+        kern[k] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
+    # per-step share: qkv/o/gate_up/down/attention once per layer, lm_head once
+    share = {k: v["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k, v in kern.items()}
+    dom = max(share, key=share.get)
+    step_ms = lm_decode / max(dec_steps, 1)
+    kv_ctx_bytes = B * arch.kv_bytes_per_token() * ctx_mid
+    step_bytes = arch.weight_bytes_per_step() + kv_ctx_bytes
+    roofline = dict(bound="hbm", kernel=f"wgemm/{dom}" if dom != "attention" else "attn_decode",
+                    achieved=round(kern[dom]["gbs"], 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(kern[dom]["gbs"] / HBM_PEAK_GBS, 4), traffic=None,
+                    bytes_per_launch=kern[dom]["bytes"], avg_launch_ms=round(kern[dom]["avg_ms"], 5),
+                    decode_step=dict(ms=round(step_ms, 4), bytes=step_bytes,
+                                     achieved_gbs=round(step_bytes / step_ms / 1e6, 1),
+                                     frac=round(step_bytes / step_ms / 1e6 / HBM_PEAK_GBS, 4)),
+                    kernels={k: dict(avg_ms=round(v["avg_ms"], 5), gbs=round(v["gbs"], 1)) for k, v in kern.items()})
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(arch, carch, prompts_all[0], N, args)
+
+    if rank == 0:
+        line = {
+            "metric": "audio-codes/sec + RTF@24kHz, TTS-1 bs=1/32, at 1/2/4/8 MI355X",
+            "value": round(codes_per_s, 2),
+            "unit": "audio-codes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init TTS-1 weights, synthetic prompt ids of the reference prompt shape)",
+            "rtf": round(rtf, 5),
+            "x_realtime": round(1.0 / rtf * B, 2),
+            "lm_prefill_ms": round(lm_prefill / args.steps, 3),
+            "lm_decode_ms": round(lm_decode / args.steps, 3),
+            "config": {
+                "workload": f"{arch.name} bf16 bs={B}/GPU: prompt {P} tokens ({args.prompt_codes} codes), "
+                            f"{N} greedy codes, codec {carch.name} on {codes_per_utt} codes",
+                "model": "TTS-1 (Llama-3.2-1B dims, V=193856, tied) + xcodec2-style codec 24 kHz",
+                "global_batch": B * world,
+                "seq_len": P + N,
+                "parallelism": f"dp{world}",
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(arch, carch, prompt, N, args):
+    """The CPU oracle (a port of the reference path) on the host cores: a bounded sample
+    of the same workload (prefill of the same prompt + `cpu_steps` greedy steps, and the
+    codec on a proportional number of codes), scaled to codes/s for the full job."""
+    from oracle import codec_oracle, lm_oracle
+    from tts_amd import synth
+
+    threads = torch.get_num_threads()
+    t0 = time.time()
+    w = synth.lm_weights_cpu(arch, 0x5EED)
+    orc = lm_oracle.LlamaOracle(arch, {k: v.float() for k, v in w.items()}, max_seq_len=len(prompt) + N + 16,
+                                dtype=torch.float32)  # fp32 weights: no per-step conversion
+    del w
+    log(f"cpu baseline: weights ready in {time.time() - t0:.1f}s, {threads} threads")
+    S = args.cpu_steps
+    t1 = time.perf_counter()
+    cache = []
+    x = orc.forward(prompt, 0, cache)
+    t_prefill = time.perf_counter() - t1
+    seq = list(prompt)
+    t2 = time.perf_counter()
+    for i in range(S):
+        sc = orc.process(orc.logits(x[-1:])[0], seq, 1.1, i, N, -1)
+        tok = int(torch.argmax(sc))
+        seq.append(tok)
+        x = orc.forward([tok], len(seq) - 1, cache)
+    t_dec = (time.perf_counter() - t2) / S
+    cw = synth.codec_weights_cpu(carch, 0xC0DEC)
+    T_s = 65
+    t3 = time.perf_counter()
+    codec_oracle.decode(cw, torch.randint(0, 65536, (T_s,)), carch.hop_length, carch.upsample_factors,
+                        carch.kernel_sizes, carch.depth)
+    t_codec_per_code = (time.perf_counter() - t3) / T_s
+    full = t_prefill + N * t_dec + (args.prompt_codes + N) * t_codec_per_code
+    return {
+        "value": round(N / full, 3),
+        "unit": "audio-codes/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle (fp32 port of HF LlamaForCausalLM greedy + reference codec): prefill {len(prompt)} "
+                   f"tokens ({t_prefill:.2f}s) + {S} decode steps ({t_dec * 1000:.1f} ms/code) + codec on {T_s} "
+                   f"codes ({t_codec_per_code * 1000:.2f} ms/code), extrapolated to the {N}-code job"),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,187 @@
+/*
+ * tts_mi355x.h — C ABI of the MI355X-native SpeechLM-TTS inference engine.
+ *
+ * This is the drop-in boundary for the `tts.inference` hot path of the reference
+ * (ishine/tts-max).  The reference has no native code: its hot path is Python calling
+ * third-party CUDA kernels.  Each entry point below replaces one reference interface:
+ *
+ *   tts_generate        replaces  model.generate(input_ids, max_length, min_new_tokens,
+ *                                  eos_token_id, do_sample, repetition_penalty, top_p,
+ *                                  temperature)     — tts/inference/inferencing.py:94-107
+ *                                  (HF GenerationMixin._sample, transformers generation/utils.py)
+ *   tts_lm_load         replaces  AutoModelForCausalLM.from_pretrained(dir, torch_dtype=...)
+ *                                  — tools/serving/inference.py:103-107 (weights come in as
+ *                                  host tensors named by their HF state-dict key)
+ *   tts_codec_load      replaces  decoder.Decoder(...).load_from_checkpoint
+ *                                  — tts/core/codec/decoder.py:17-67, 91-119
+ *   tts_codec_decode    replaces  AudioDecoder.decode(speech_ids) -> Decoder.forward
+ *                                  — tts/core/codec/decoding.py:84-89, decoder.py:69-89
+ *
+ * Conventions
+ *   - Every function returns tts_status (0 = TTS_OK).  On error the message is available
+ *     from tts_last_error() (thread-local).  No C++ exception crosses this boundary.
+ *   - Plain pointers and sizes only.  `stream` is a hipStream_t passed as void* (NULL =
+ *     the engine's own stream).  Pointers documented "device" must be device memory of the
+ *     engine's GPU; "host" pointers are ordinary CPU memory.
+ *   - One engine = one GPU.  An engine is not re-entrant: use one engine per thread/GPU.
+ *   - The engine owns weights, KV cache, workspaces and captured hipGraphs; the caller owns
+ *     every buffer it passes in.
+ */
+#ifndef TTS_MI355X_H
+#define TTS_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTS_ABI_VERSION 1
+
+typedef int32_t tts_status;
+enum {
+  TTS_OK = 0,
+  TTS_E_INVALID = 1,     /* bad argument / shape / missing tensor              */
+  TTS_E_HIP = 2,         /* HIP runtime error                                  */
+  TTS_E_OOM = 3,         /* device allocation failed                           */
+  TTS_E_STATE = 4,       /* call order violated (e.g. generate before load)    */
+  TTS_E_UNSUPPORTED = 5  /* configuration not implemented                      */
+};
+
+enum { TTS_DT_F32 = 0, TTS_DT_BF16 = 1, TTS_DT_F16 = 2, TTS_DT_I32 = 3, TTS_DT_I64 = 4 };
+
+typedef struct tts_engine tts_engine;
+
+/* One named host tensor (row-major, contiguous).  Names are the reference state-dict keys:
+ * HF Llama keys for the SpeechLM ("model.layers.3.mlp.up_proj.weight", ...) and the codec
+ * Decoder keys ("decoder.backbone.embed.weight", "fc_post_a.bias", ...). */
+typedef struct {
+  const char* name;
+  const void* data;
+  int32_t dtype;
+  int32_t ndim;
+  int64_t shape[4];
+  int32_t on_device; /* 0: `data` is host memory; 1: device memory of the engine's GPU */
+} tts_tensor_desc;
+
+/* ---------------------------------------------------------------- engine lifecycle --- */
+
+int32_t tts_abi_version(void);
+const char* tts_last_error(void);
+tts_status tts_engine_create(int32_t device, tts_engine** out);
+void tts_engine_destroy(tts_engine* e);
+
+/* ------------------------------------------------------------------------- SpeechLM --- */
+
+/* LlamaForCausalLM architecture (transformers models/llama/configuration_llama.py). */
+typedef struct {
+  int32_t hidden_size;         /* 2048 (TTS-1) / 4096 (TTS-1-Max)                    */
+  int32_t num_layers;          /* 16 / 32                                            */
+  int32_t num_heads;           /* 32                                                 */
+  int32_t num_kv_heads;        /* 8                                                  */
+  int32_t head_dim;            /* 64 / 128                                           */
+  int32_t intermediate_size;   /* 8192 / 14336                                       */
+  int32_t vocab_size;          /* 193856                                             */
+  int32_t tie_word_embeddings; /* 1 for TTS-1                                        */
+  float rms_norm_eps;          /* 1e-5                                               */
+  float rope_theta;            /* 500000                                             */
+  int32_t rope_llama3;         /* 1: llama3 frequency smoothing                      */
+  float rope_factor;           /* 32 (TTS-1) / 8 (TTS-1-Max)                         */
+  float rope_low_freq_factor;  /* 1                                                  */
+  float rope_high_freq_factor; /* 4                                                  */
+  int32_t rope_original_max_position; /* 8192                                        */
+  int32_t max_batch;           /* KV-cache slots (sequences resident at once)        */
+  int32_t max_seq_len;         /* KV capacity per sequence (prompt + generated)      */
+} tts_lm_config;
+
+/* Loads the SpeechLM.  Weights are bf16 (or f32 / f16, converted to bf16 on load).
+ * Optional tensors "rope.cos" / "rope.sin" ([max_seq_len, head_dim], bf16) override the
+ * engine-computed RoPE table (the Python host passes the table computed exactly as
+ * LlamaRotaryEmbedding.forward does).  Optional "vocab.id_to_code" (int32 [vocab]) is the
+ * token-id -> speech-code LUT (-1 for non-speech ids), see tts_lm_id_to_code. */
+tts_status tts_lm_load(tts_engine* e, const tts_lm_config* cfg, const tts_tensor_desc* t,
+                       int32_t n);
+
+/* Generation parameters: the HF `generate` kwargs of inferencing.py:95-104. */
+typedef struct {
+  int32_t max_length;          /* TOTAL length incl. prompt (HF max_length)          */
+  int32_t min_new_tokens;      /* EOS masked until this many new tokens exist        */
+  int32_t eos_token_id;        /* <|speech_end|>; -1 = none                          */
+  int32_t do_sample;           /* 0 = greedy (argmax, lowest index on ties)          */
+  float repetition_penalty;    /* over the SET of ids in prompt+generated            */
+  float temperature;           /* sampling only                                      */
+  float top_p;                 /* sampling only                                      */
+  int32_t top_k;               /* sampling only (HF default 50); 0 = off             */
+  uint64_t seed;               /* sampling RNG seed                                  */
+} tts_gen_params;
+
+/* Runs prefill + the autoregressive decode loop for `batch` independent sequences.
+ *   prompt_ids  host int32, the prompts concatenated            [sum(prompt_lens)]
+ *   prompt_lens host int32                                      [batch]
+ *   out_ids     host int32, NEW tokens per sequence, row stride `out_stride`
+ *               (EOS included when produced, as HF returns it)  [batch][out_stride]
+ *   out_lens    host int32, number of new tokens per sequence   [batch]
+ * Each sequence is computed exactly as a batch-1 HF generate of that prompt would be
+ * (ragged batching: no padding enters the arithmetic). */
+tts_status tts_generate(tts_engine* e, const tts_gen_params* p, const int32_t* prompt_ids,
+                        const int32_t* prompt_lens, int32_t batch, int32_t* out_ids,
+                        int32_t out_stride, int32_t* out_lens, void* stream);
+
+/* Teacher-forced scoring (parity / debugging): runs the prefill over full sequences and
+ * writes the bf16-rounded logits of the last `n_last` positions of each sequence, as
+ * fp32, to host `logits` [batch][n_last][vocab]. */
+tts_status tts_lm_score(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
+                        int32_t n_last, float* logits, void* stream);
+
+/* Maps token ids to speech codes through the loaded LUT (-1 for non-speech ids). */
+tts_status tts_lm_id_to_code(tts_engine* e, const int32_t* ids, int32_t n, int32_t* codes);
+
+/* Device time of the last tts_generate, split in prefill / decode (milliseconds), and the
+ * number of decode steps executed. */
+tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms,
+                              int32_t* decode_steps);
+
+/* Times one decode-step kernel of the loaded model in isolation (HIP events on the engine
+ * stream around `iters` back-to-back launches, after one warm-up launch) for roofline
+ * accounting.  which: 0 qkv projection (+RMSNorm), 1 o_proj (+residual), 2 gate/up
+ * (+RMSNorm, SwiGLU), 3 down_proj (+residual), 4 lm_head (+RMSNorm, penalty, argmax
+ * partials), 5 decode attention (ctx = `ctx` positions).  rows = batch rows.
+ * Outputs: average ms per launch and the algorithmic HBM bytes one launch must move. */
+tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
+                               int32_t iters, float* avg_ms, double* bytes);
+
+/* ---------------------------------------------------------------------- codec ------ */
+
+/* xcodec2-compatible decoder (tts/core/codec/decoding.py:14-35 DecoderConfig). */
+typedef struct {
+  int32_t sample_rate;         /* 16000 / 24000 / 48000                               */
+  int32_t token_rate;          /* 50                                                  */
+  int32_t hop_length;          /* 320 / 160                                           */
+  int32_t n_upsample;          /* len(upsample_factors), 0..4                         */
+  int32_t upsample_factors[4];
+  int32_t kernel_sizes[4];
+  int32_t hidden_dim;          /* 1024                                                */
+  int32_t depth;               /* 12 transformer blocks                               */
+  int32_t heads;               /* 16                                                  */
+  int32_t vq_dim;              /* 2048                                                */
+  int32_t max_codes;           /* largest T the workspaces are sized for              */
+} tts_codec_config;
+
+tts_status tts_codec_load(tts_engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t,
+                          int32_t n);
+
+/* Decodes `batch` code sequences (host int32, concatenated, lengths in `lens`) into
+ * waveforms.  wav: float32 [sum(lens) * samples_per_code] concatenated in input order;
+ * wav_is_device != 0 means `wav` is a device pointer.  wav_lens (host) receives each
+ * utterance's sample count. */
+tts_status tts_codec_decode(tts_engine* e, const int32_t* codes, const int32_t* lens,
+                            int32_t batch, float* wav, int32_t wav_is_device, int64_t* wav_lens,
+                            void* stream);
+
+tts_status tts_codec_samples_per_code(tts_engine* e, int32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTS_MI355X_H */

@@ -1,0 +1,47 @@
+/*
+ * tts_mi355x_ops.h — op-level entry points of the same library, used by the parity tests
+ * to check each kernel family in isolation against the CPU oracle.  All pointers are
+ * device pointers of the current HIP device; `stream` is a hipStream_t (NULL = default).
+ * These are not part of the drop-in surface (tts_mi355x.h) and may change between rounds.
+ */
+#ifndef TTS_MI355X_OPS_H
+#define TTS_MI355X_OPS_H
+
+#include <stdint.h>
+#include "tts_mi355x.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Deterministic synthetic weights: value_i = (2*u_i - 1) * scale, u_i = top 24 bits of
+ * splitmix64(seed + (i+1)*golden) / 2^24.  dtype TTS_DT_F32 or TTS_DT_BF16 (RNE).  Bit-identical
+ * to tts_amd.synth.synth_values (numpy). */
+tts_status tts_synth_fill(void* dst, int32_t dtype, int64_t n, uint64_t seed, float scale,
+                          void* stream);
+
+/* W [N][K] bf16 row-major -> 1 KiB MFMA fragment tiles (layout in lm_gemm.hip). */
+tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, void* stream);
+
+/* y[M][ldo] (bf16) = epilogue( A[M][K] . W^T ), A optionally RMSNorm'ed with normw.
+ * epi: 0 store, 1 residual (resid += y, in place), 2 SwiGLU (W = interleaved gate/up tiles,
+ * N = 2*intermediate, output [M][N/2]).  M <= 64. */
+tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w_tiled,
+                        int32_t N, const void* normw, float eps, void* out, int32_t ldo,
+                        void* resid, int32_t epi, void* stream);
+
+/* LlamaRMSNorm over rows of x (bf16). */
+tts_status tts_op_rmsnorm(const void* x, const void* w, float eps, void* y, int32_t M, int32_t K,
+                          void* stream);
+
+/* fp32 GEMM on the codec path: C[M][N] = act(A[M][K] . B[N][K]^T + bias) (+ resid).
+ * lda may be < K to express a sliding-window (im2col-free) conv operand.  act: 0 none,
+ * 1 swish, 2 silu (same function), see codec_gemm.hip. */
+tts_status tts_op_gemm_f32(const float* A, int32_t M, int32_t K, int32_t lda, const float* B,
+                           int32_t N, const float* bias, float* C, int32_t ldc,
+                           const float* resid, int32_t act, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTS_MI355X_OPS_H */

@@ -1,0 +1,159 @@
+"""Op-level parity of the HIP kernels (through the C ABI) against the CPU oracle ops.
+
+Tolerances: bf16 outputs may differ from the fp32-accumulated oracle by a different
+summation order only, i.e. by at most a couple of bf16 ulps on a small fraction of
+elements; fp32 codec GEMMs to ~1e-5 relative.
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import lm_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from tts_amd import _lib
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return _lib.load_library()
+
+
+def _check(st):
+    from tts_amd import _lib
+
+    _lib.check(st)
+
+
+def _bf16_close(got, ref, max_ulps=2, frac=0.01):
+    """Elementwise within max_ulps bf16 ulps, and at most `frac` of elements differ at all."""
+    g, r = got.float(), ref.float()
+    ulp = torch.clamp(r.abs(), min=1e-30) * 2.0 ** -7
+    bad = (g - r).abs() > max_ulps * ulp + 1e-6
+    assert bad.sum().item() == 0, f"{bad.sum().item()} elements beyond {max_ulps} ulps"
+    ndiff = (g != r).float().mean().item()
+    assert ndiff <= frac, f"{ndiff:.4f} of elements differ"
+
+
+def test_synth_fill_bit_identical(lib):
+    from tts_amd import synth, _lib
+
+    for n, seed, scale in [(1000, 1, 0.5), (4097, 0xDEADBEEF12345, 0.0346)]:
+        ref = synth.synth_values(seed, n, scale)
+        d = torch.empty(n, dtype=torch.float32, device="cuda")
+        _check(lib.tts_synth_fill(d.data_ptr(), _lib.DT_F32, n, seed, scale, None))
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        b = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        _check(lib.tts_synth_fill(b.data_ptr(), _lib.DT_BF16, n, seed, scale, None))
+        torch.cuda.synchronize()
+        assert torch.equal(b.cpu(), torch.from_numpy(ref).to(torch.bfloat16))
+
+
+def _tiled(lib, w):
+    N, K = w.shape
+    t = torch.empty_like(w)
+    _check(lib.tts_op_retile(w.data_ptr(), t.data_ptr(), N, K, None))
+    return t
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 40, 64])
+@pytest.mark.parametrize("N,K", [(256, 256), (3072, 2048), (2048, 8192)])
+def test_wgemm_store(lib, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.02).to(torch.bfloat16)
+    ref = lm_oracle.linear(x, w)
+    xd, wd = x.cuda(), w.cuda()
+    wt = _tiled(lib, wd)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    _check(lib.tts_op_wgemm(xd.data_ptr(), M, K, K, wt.data_ptr(), N, None, 0.0, out.data_ptr(), N, None, 0, None))
+    torch.cuda.synchronize()
+    _bf16_close(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("M", [1, 4, 16])
+def test_wgemm_norm_resid_swiglu(lib, M):
+    K, FF = 2048, 1024
+    g = torch.Generator().manual_seed(M)
+    x = (torch.randn(M, K, generator=g)).to(torch.bfloat16)
+    nw = (1 + 0.2 * torch.randn(K, generator=g)).to(torch.bfloat16)
+    wg = (torch.randn(FF, K, generator=g) * 0.02).to(torch.bfloat16)
+    wu = (torch.randn(FF, K, generator=g) * 0.02).to(torch.bfloat16)
+    h = lm_oracle.rmsnorm(x, nw, 1e-5)
+    ref_act = torch.nn.functional.silu(lm_oracle.linear(h, wg)) * lm_oracle.linear(h, wu)
+    # interleaved gate/up tiles, as the engine lays out mlp.gate_proj / mlp.up_proj
+    gt, ut = _tiled(lib, wg.cuda()), _tiled(lib, wu.cuda())
+    KT = K // 32
+    wgu = torch.stack([gt.view(FF // 16, KT * 512), ut.view(FF // 16, KT * 512)], 1).reshape(2 * FF, K).contiguous()
+    out = torch.empty(M, FF, dtype=torch.bfloat16, device="cuda")
+    xd, nd = x.cuda(), nw.cuda()
+    _check(lib.tts_op_wgemm(xd.data_ptr(), M, K, K, wgu.data_ptr(), 2 * FF, nd.data_ptr(), 1e-5, out.data_ptr(), FF,
+                            None, 2, None))
+    torch.cuda.synchronize()
+    _bf16_close(out.cpu(), ref_act, max_ulps=3, frac=0.03)
+    # residual epilogue: resid += act . Wd^T
+    wd = (torch.randn(K, FF, generator=g) * 0.02).to(torch.bfloat16)
+    ref_res = x + lm_oracle.linear(ref_act, wd)
+    wdt = _tiled(lib, wd.cuda())
+    res = xd.clone()
+    act = ref_act.cuda()
+    _check(lib.tts_op_wgemm(act.data_ptr(), M, FF, FF, wdt.data_ptr(), K, None, 0.0, None, K, res.data_ptr(), 1, None))
+    torch.cuda.synchronize()
+    _bf16_close(res.cpu(), ref_res, max_ulps=2, frac=0.02)
+
+
+def test_rmsnorm(lib):
+    M, K = 7, 2048
+    x = torch.randn(M, K).to(torch.bfloat16)
+    w = (1 + 0.2 * torch.randn(K)).to(torch.bfloat16)
+    ref = lm_oracle.rmsnorm(x, w, 1e-5)
+    xd, wd = x.cuda(), w.cuda()
+    y = torch.empty_like(xd)
+    _check(lib.tts_op_rmsnorm(xd.data_ptr(), wd.data_ptr(), 1e-5, y.data_ptr(), M, K, None))
+    torch.cuda.synchronize()
+    _bf16_close(y.cpu(), ref, max_ulps=1, frac=0.01)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 16), (65, 130, 48), (300, 1024, 2048), (129, 642, 656)])
+def test_gemm_f32(lib, M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    for act in (0, 1):
+        ref = A.double() @ B.double().t() + bias.double()
+        if act:
+            ref = ref * torch.sigmoid(ref)
+        ref = ref + R.double()
+        Ad, Bd, bd, Rd = A.cuda(), B.cuda(), bias.cuda(), R.cuda()
+        C = torch.empty(M, N, device="cuda")
+        _check(lib.tts_op_gemm_f32(Ad.data_ptr(), M, K, K, Bd.data_ptr(), N, bd.data_ptr(), C.data_ptr(), N,
+                                   Rd.data_ptr(), act, None))
+        torch.cuda.synchronize()
+        err = (C.cpu().double() - ref).abs().max().item()
+        assert err <= 2e-6 * (A.abs() @ B.abs().t()).max().item() + 1e-5, err
+
+
+def test_gemm_f32_sliding_window_conv(lib):
+    """Conv1d(k=3, pad=1) as a GEMM over a zero-padded time-major buffer (lda = C < K)."""
+    T, C, Co, k = 37, 64, 48, 3
+    x = torch.randn(1, C, T)
+    w = torch.randn(Co, C, k) * 0.1
+    b = torch.randn(Co)
+    ref = torch.nn.functional.conv1d(x, w, b, padding=1)[0].t()  # [T, Co]
+    xp = torch.zeros(T + 2, C)
+    xp[1:T + 1] = x[0].t()
+    wr = w.permute(0, 2, 1).reshape(Co, k * C).contiguous()  # [co][j*C + ci]
+    xd, wd, bd = xp.cuda(), wr.cuda(), b.cuda()
+    out = torch.empty(T, Co, device="cuda")
+    _check(lib.tts_op_gemm_f32(xd.data_ptr(), T, k * C, C, wd.data_ptr(), Co, bd.data_ptr(), out.data_ptr(), Co,
+                               None, 0, None))
+    torch.cuda.synchronize()
+    assert torch.allclose(out.cpu(), ref, atol=1e-4, rtol=1e-4)

@@ -1,0 +1,235 @@
+// capi.cpp — the extern "C" boundary (include/tts_mi355x.h, include/tts_mi355x_ops.h).
+// Every entry point catches everything: errors become a status code plus a thread-local
+// message, never an exception across the ABI.
+#include <string>
+
+#include "../../include/tts_mi355x.h"
+#include "../../include/tts_mi355x_ops.h"
+#include "codec_kernels.h"
+#include "engine.h"
+
+namespace tts {
+
+static thread_local std::string g_last_error;
+
+template <class F>
+static tts_status guarded(F&& f) {
+  try {
+    f();
+    return TTS_OK;
+  } catch (const Error& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return TTS_E_INVALID;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return TTS_E_INVALID;
+  }
+}
+
+hipStream_t pick_stream(Engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
+
+Engine::~Engine() {
+  if (w.graph) hipGraphExecDestroy(w.graph);
+  if (w.h_active) hipHostFree(w.h_active);
+  if (codec) codec_destroy(codec);
+  for (auto& v : ev)
+    if (v) hipEventDestroy(v);
+  if (stream) hipStreamDestroy(stream);
+}
+
+}  // namespace tts
+
+using namespace tts;
+
+extern "C" {
+
+int32_t tts_abi_version(void) { return TTS_ABI_VERSION; }
+
+const char* tts_last_error(void) { return g_last_error.c_str(); }
+
+tts_status tts_engine_create(int32_t device, tts_engine** out) {
+  return guarded([&] {
+    TTS_REQUIRE(out != nullptr, "null output pointer");
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    TTS_REQUIRE(device >= 0 && device < n, "device index out of range");
+    HIP_CHECK(hipSetDevice(device));
+    Engine* e = new Engine();
+    e->device = device;
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    e->num_cu = prop.multiProcessorCount;
+    HIP_CHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    for (auto& v : e->ev) HIP_CHECK(hipEventCreate(&v));
+    *out = reinterpret_cast<tts_engine*>(e);
+  });
+}
+
+void tts_engine_destroy(tts_engine* e) {
+  if (!e) return;
+  Engine* E = reinterpret_cast<Engine*>(e);
+  hipSetDevice(E->device);
+  hipDeviceSynchronize();
+  delete E;
+}
+
+tts_status tts_lm_load(tts_engine* e, const tts_lm_config* cfg, const tts_tensor_desc* t,
+                       int32_t n) {
+  return guarded([&] {
+    TTS_REQUIRE(e && t && n > 0, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_load(E, cfg, t, n);
+  });
+}
+
+tts_status tts_generate(tts_engine* e, const tts_gen_params* p, const int32_t* prompt_ids,
+                        const int32_t* prompt_lens, int32_t batch, int32_t* out_ids,
+                        int32_t out_stride, int32_t* out_lens, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(e && out_ids && out_lens, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_generate(E, p, prompt_ids, prompt_lens, batch, out_ids, out_stride, out_lens,
+                pick_stream(E, stream));
+  });
+}
+
+tts_status tts_lm_score(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
+                        int32_t n_last, float* logits, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(e && ids && lens && logits && n_last >= 1, "bad argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_score(E, ids, lens, batch, n_last, logits, pick_stream(E, stream));
+  });
+}
+
+tts_status tts_lm_id_to_code(tts_engine* e, const int32_t* ids, int32_t n, int32_t* codes) {
+  return guarded([&] {
+    TTS_REQUIRE(e && ids && codes && n >= 0, "bad argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    TTS_REQUIRE(!E->lm.id_to_code.empty(), "no vocab.id_to_code LUT was loaded");
+    const int V = (int)E->lm.id_to_code.size();
+    for (int i = 0; i < n; ++i) codes[i] = (ids[i] >= 0 && ids[i] < V) ? E->lm.id_to_code[ids[i]] : -1;
+  });
+}
+
+tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms,
+                              int32_t* decode_steps) {
+  return guarded([&] {
+    TTS_REQUIRE(e, "null engine");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    if (prefill_ms) *prefill_ms = E->t_prefill_ms;
+    if (decode_ms) *decode_ms = E->t_decode_ms;
+    if (decode_steps) *decode_steps = E->decode_steps;
+  });
+}
+
+tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
+                               int32_t iters, float* avg_ms, double* bytes) {
+  return guarded([&] {
+    TTS_REQUIRE(e && avg_ms && bytes, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_bench_kernel(E, which, rows, ctx, iters, avg_ms, bytes);
+  });
+}
+
+tts_status tts_codec_load(tts_engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t,
+                          int32_t n) {
+  return guarded([&] {
+    TTS_REQUIRE(e && cfg && t && n > 0, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    codec_load(E, cfg, t, n);
+  });
+}
+
+tts_status tts_codec_decode(tts_engine* e, const int32_t* codes, const int32_t* lens,
+                            int32_t batch, float* wav, int32_t wav_is_device, int64_t* wav_lens,
+                            void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(e && codes && lens && wav && wav_lens && batch >= 1, "bad argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    codec_decode(E, codes, lens, batch, wav, wav_is_device, wav_lens, pick_stream(E, stream));
+  });
+}
+
+tts_status tts_codec_samples_per_code(tts_engine* e, int32_t* out) {
+  return guarded([&] {
+    TTS_REQUIRE(e && out, "null argument");
+    *out = codec_samples_per_code(reinterpret_cast<Engine*>(e));
+  });
+}
+
+// ------------------------------------------------------------------------ op level ----
+
+tts_status tts_synth_fill(void* dst, int32_t dtype, int64_t n, uint64_t seed, float scale,
+                          void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(dst && n >= 0 && (dtype == TTS_DT_F32 || dtype == TTS_DT_BF16), "bad argument");
+    launch_synth_fill(dst, dtype == TTS_DT_F32 ? 0 : 1, n, seed, scale, (hipStream_t)stream);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(w && w_tiled && N % 16 == 0 && K % 32 == 0, "bad argument");
+    launch_retile((const bf16_t*)w, (bf16_t*)w_tiled, N, K, (hipStream_t)stream, 1, 0);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w_tiled,
+                        int32_t N, const void* normw, float eps, void* out, int32_t ldo,
+                        void* resid, int32_t epi, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(epi == EPI_STORE || epi == EPI_RESID || epi == EPI_SWIGLU, "bad epilogue");
+    TTS_REQUIRE(wgemm_supported(M, N, K, epi), "unsupported GEMM shape");
+    TTS_REQUIRE(ldx == K, "ldx must equal K");
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+    WgemmPlan p = plan_wgemm(M, N, K, epi, prop.multiProcessorCount);
+    TTS_REQUIRE(normw == nullptr || p.a_lds, "fused RMSNorm needs M*K small enough for LDS");
+    WgemmArgs a;
+    a.x = (const bf16_t*)x; a.M = M; a.K = K; a.ldx = ldx;
+    a.w = (const bf16_t*)w_tiled; a.N = N;
+    a.normw = (const bf16_t*)normw; a.eps = eps;
+    a.out = (bf16_t*)out; a.ldo = ldo; a.resid = (bf16_t*)resid;
+    launch_wgemm(a, p, epi, normw != nullptr, (hipStream_t)stream);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+tts_status tts_op_rmsnorm(const void* x, const void* w, float eps, void* y, int32_t M, int32_t K,
+                          void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(x && w && y && K % 8 == 0, "bad argument");
+    launch_rmsnorm((const bf16_t*)x, K, (const bf16_t*)w, eps, (bf16_t*)y, K, M, K,
+                   (hipStream_t)stream);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+tts_status tts_op_gemm_f32(const float* A, int32_t M, int32_t K, int32_t lda, const float* B,
+                           int32_t N, const float* bias, float* C, int32_t ldc,
+                           const float* resid, int32_t act, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0, "bad argument");
+    GemmF32Args g;
+    g.A = A; g.M = M; g.K = K; g.lda = lda; g.B = B; g.N = N; g.bias = bias;
+    g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
+    launch_gemm_f32(g, (hipStream_t)stream);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

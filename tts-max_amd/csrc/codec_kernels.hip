@@ -1,0 +1,463 @@
+// codec_kernels.hip — fp32 kernels of the xcodec2-compatible codec decoder.
+//
+// Reference: tts/core/codec/decoder.py:69-89 (Decoder.forward) and decoder_modules.py
+// (ISTFT 19-93, ISTFTHead 96-148, ResnetBlock 162-223, RMSNorm 226-236, MLP 239-251,
+// Attention 254-290, TransformerBlock 293-314, VocosBackbone 317-400), upsampler.py 9-69.
+// The reference runs the codec in fp32; so does this path: every contraction is a
+// v_mfma_f32_32x32x2_f32 GEMM (exact fp32 products, fp32 accumulation).
+//
+// MI355X layout: activations are time-major [T][C] (row = one frame, channels contiguous),
+// so a Conv1d(k) over a zero-padded buffer is a plain GEMM whose A operand is a sliding
+// window: row t starts at x + (t - k/2)*C and spans k*C contiguous floats (lda = C < K).
+// No im2col buffer is ever written.
+#include "codec_kernels.h"
+#include "hip_common.h"
+
+namespace tts {
+
+// ------------------------------------------------------------------ fp32 MFMA GEMM ----
+constexpr int GBM = 128, GBN = 128, GBK = 16;
+constexpr int GLS = 130;  // LDS row stride (floats): conflict-free transposed stores
+
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
+  __shared__ float As[GBK * GLS];
+  __shared__ float Bs[GBK * GLS];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware tile order: consecutive tiles of one A row-block go to one XCD (speed only)
+  const int nbn = (g.N + GBN - 1) / GBN;
+  const int bid = blockIdx.x;
+  const int m0 = (bid / nbn) * GBM, n0 = (bid % nbn) * GBN;
+  // global->LDS staging map: thread loads 8 consecutive k of one row (2 x float4)
+  const int lrow = t >> 1, lk = (t & 1) * 8;
+  const int ar = m0 + lrow, br = n0 + lrow;
+  const float* ap = g.A + (size_t)ar * g.lda + lk;
+  const float* bp = g.B + (size_t)br * g.K + lk;
+  const bool aok = ar < g.M, bok = br < g.N;
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 ra0, ra1, rb0, rb1;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  ra0 = aok ? *(const float4*)(ap) : z4;
+  ra1 = aok ? *(const float4*)(ap + 4) : z4;
+  rb0 = bok ? *(const float4*)(bp) : z4;
+  rb1 = bok ? *(const float4*)(bp + 4) : z4;
+  for (int k0 = 0; k0 < g.K; k0 += GBK) {
+    __syncthreads();
+    const float av[8] = {ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w};
+    const float bv[8] = {rb0.x, rb0.y, rb0.z, rb0.w, rb1.x, rb1.y, rb1.z, rb1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      As[(lk + j) * GLS + lrow] = av[j];
+      Bs[(lk + j) * GLS + lrow] = bv[j];
+    }
+    __syncthreads();
+    if (k0 + GBK < g.K) {  // prefetch next K tile while the MFMAs run
+      const int kn = k0 + GBK;
+      ra0 = aok ? *(const float4*)(ap + kn) : z4;
+      ra1 = aok ? *(const float4*)(ap + kn + 4) : z4;
+      rb0 = bok ? *(const float4*)(bp + kn) : z4;
+      rb1 = bok ? *(const float4*)(bp + kn + 4) : z4;
+    }
+#pragma unroll
+    for (int kk = 0; kk < GBK / 2; ++kk) {
+      const int kr = 2 * kk + (lane >> 5);
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[kr * GLS + wm * 64 + i * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[kr * GLS + wn * 64 + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+    if (n >= g.N) continue;
+    const float bias = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;
+        float v = acc[i][j][r] + bias;
+        if (g.act == 1) v = v / (1.0f + expf(-v));
+        if (g.resid) v = g.resid[(size_t)m * g.ldc + n] + v;
+        g.C[(size_t)m * g.ldc + n] = v;
+      }
+  }
+}
+
+void launch_gemm_f32(const GemmF32Args& g, hipStream_t s) {
+  const int grid = ((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN);
+  hipLaunchKernelGGL(gemm_f32_kernel, dim3(grid), dim3(256), 0, s, g);
+}
+
+// ------------------------------------------------------------------ small kernels -----
+// ResidualFSQ(levels=[4]*8, num_quantizers=1).get_output_from_indices
+// (vector_quantize_pytorch 1.17.8): digit_j = (i // 4^j) % 4, code_j = (digit_j - 2) / 2,
+// scale 1 for quantizer 0, then project_out Linear(8 -> vq_dim).
+__global__ void fsq_project_kernel(const int* __restrict__ codes, const float* __restrict__ w,
+                                   const float* __restrict__ b, float* __restrict__ out, int vq) {
+  const int t = blockIdx.x;
+  const int c = codes[t];
+  float z[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (float)(((c >> (2 * j)) & 3) - 2) * 0.5f;
+  for (int o = threadIdx.x; o < vq; o += blockDim.x) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += z[j] * w[o * 8 + j];
+    out[(size_t)t * vq + o] = acc + b[o];
+  }
+}
+
+void launch_fsq_project(const int* codes, int T, const float* w, const float* b, float* out,
+                        int vq_dim, hipStream_t s) {
+  hipLaunchKernelGGL(fsq_project_kernel, dim3(T), dim3(256), 0, s, codes, w, b, out, vq_dim);
+}
+
+// GroupNorm statistics (torch.nn.GroupNorm, biased variance), two passes in fp32.
+__global__ void groupnorm_stats_kernel(const float* __restrict__ x, int T, int C, int cg,
+                                       float eps, float* __restrict__ stats) {
+  __shared__ float red[16];
+  const int grp = blockIdx.x;
+  const long long n = (long long)T * cg;
+  float sum = 0.f;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+    const int t = (int)(i / cg), c = (int)(i % cg);
+    sum += x[(size_t)t * C + grp * cg + c];
+  }
+  const float mean = block_sum(sum, red) / (float)n;
+  float sq = 0.f;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+    const int t = (int)(i / cg), c = (int)(i % cg);
+    const float d = x[(size_t)t * C + grp * cg + c] - mean;
+    sq += d * d;
+  }
+  const float var = block_sum(sq, red) / (float)n;
+  if (threadIdx.x == 0) {
+    stats[2 * grp] = mean;
+    stats[2 * grp + 1] = 1.0f / sqrtf(var + eps);
+  }
+}
+
+void launch_groupnorm_stats(const float* x, int T, int C, int groups, float eps, float* stats,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(groups), dim3(1024), 0, s, x, T, C,
+                     C / groups, eps, stats);
+}
+
+__global__ void groupnorm_swish_kernel(const float* __restrict__ x, int T, int C, int cg,
+                                       const float* __restrict__ stats,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float* __restrict__ y) {
+  const long long n = (long long)T * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C), grp = c / cg;
+    const float v = (x[i] - stats[2 * grp]) * stats[2 * grp + 1] * gamma[c] + beta[c];
+    y[i] = v / (1.0f + expf(-v));
+  }
+}
+
+void launch_groupnorm_swish(const float* x, int T, int C, int groups, const float* stats,
+                            const float* gamma, const float* beta, float* y, hipStream_t s) {
+  const long long n = (long long)T * C;
+  int grid = (int)std::min<long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(groupnorm_swish_kernel, dim3(grid), dim3(256), 0, s, x, T, C, C / groups,
+                     stats, gamma, beta, y);
+}
+
+__global__ void rmsnorm_f32_kernel(const float* __restrict__ x, int C, const float* __restrict__ w,
+                                   float eps, float* __restrict__ y) {
+  __shared__ float red[16];
+  const float* xr = x + (size_t)blockIdx.x * C;
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) ss += xr[c] * xr[c];
+  const float r = 1.0f / sqrtf(block_sum(ss, red) / (float)C + eps);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) y[(size_t)blockIdx.x * C + c] = xr[c] * r * w[c];
+}
+
+void launch_rmsnorm_f32(const float* x, int T, int C, const float* w, float eps, float* y,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(rmsnorm_f32_kernel, dim3(T), dim3(256), 0, s, x, C, w, eps, y);
+}
+
+__global__ void layernorm_f32_kernel(const float* __restrict__ x, int C, const float* __restrict__ w,
+                                     const float* __restrict__ b, float eps, float* __restrict__ y) {
+  __shared__ float red[16];
+  const float* xr = x + (size_t)blockIdx.x * C;
+  float s1 = 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) s1 += xr[c];
+  const float mean = block_sum(s1, red) / (float)C;
+  float s2 = 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) { const float d = xr[c] - mean; s2 += d * d; }
+  const float rstd = 1.0f / sqrtf(block_sum(s2, red) / (float)C + eps);
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    y[(size_t)blockIdx.x * C + c] = (xr[c] - mean) * rstd * w[c] + b[c];
+}
+
+void launch_layernorm_f32(const float* x, int T, int C, const float* w, const float* b, float eps,
+                          float* y, hipStream_t s) {
+  hipLaunchKernelGGL(layernorm_f32_kernel, dim3(T), dim3(256), 0, s, x, C, w, b, eps, y);
+}
+
+// torchtune RotaryPositionalEmbeddings(dim=64, base=10000) as the reference applies it to
+// [b, h, t, d] tensors: the rotated "sequence" index is the HEAD index (decoder_modules.py
+// 276-281; same quirk documented in transformers models/xcodec2).  Pairs are interleaved.
+__global__ void codec_rope_kernel(float* __restrict__ qkv, int T, int heads, int hd) {
+  const int t = blockIdx.x;
+  const int W = heads * hd;
+  for (int i = threadIdx.x; i < heads * hd; i += blockDim.x) {  // one (q or k) pair per 2
+    const int h = i / hd, d = i % hd;
+    if (d & 1) continue;
+    const int pi = d >> 1;
+    const float theta = 1.0f / powf(10000.0f, (float)(2 * pi) / (float)hd);
+    const float ang = (float)h * theta;
+    const float c = cosf(ang), s = sinf(ang);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {  // q then k
+      float* p = qkv + (size_t)t * 3 * W + r * W + h * hd + d;
+      const float x0 = p[0], x1 = p[1];
+      p[0] = x0 * c - x1 * s;
+      p[1] = x1 * c + x0 * s;
+    }
+  }
+}
+
+void launch_codec_rope(float* qkv, int T, int heads, int hd, hipStream_t s) {
+  hipLaunchKernelGGL(codec_rope_kernel, dim3(T), dim3(256), 0, s, qkv, T, heads, hd);
+}
+
+// ------------------------------------------------------------- codec attention --------
+// Non-causal SDPA (decoder_modules.py:283-285) for head_dim 64, fp32 flash attention on
+// v_mfma_f32_32x32x2_f32: one workgroup = one (head, 64-query block); keys in chunks of
+// 64 with online softmax.  Four waves own the 2x2 quadrants of every 64x64 tile.
+constexpr int AB = 64;   // query rows / key chunk
+constexpr int AD = 64;   // head dim
+constexpr int ALS = 65;  // padded LDS stride
+
+__global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict__ qkv, int T,
+                                                         int heads, float* __restrict__ out) {
+  extern __shared__ float sm[];
+  float* Qt = sm;                  // [AD][AB]   (k-major for A-operand reads)
+  float* Kt = Qt + AD * AB;        // [AD][AB]
+  float* Vs = Kt + AD * AB;        // [AB keys][AD]
+  float* Ss = Vs + AB * AD;        // [AB][ALS] scores
+  float* Pt = Ss + AB * ALS;       // [AB keys][AB rows]
+  float* mrow = Pt + AB * AB;      // [AB] running max
+  float* lrow = mrow + AB;         // [AB] running sum
+  float* arow = lrow + AB;         // [AB] rescale factor of this chunk
+  const int h = blockIdx.y, q0 = blockIdx.x * AB;
+  const int W = heads * AD, ld = 3 * W;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
+  const float scale = 0.125f;  // 1/sqrt(64)
+  // Q tile, transposed
+  for (int i = t; i < AB * AD / 4; i += 256) {
+    const int r = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q0 + r < T) v = *(const float4*)(qkv + (size_t)(q0 + r) * ld + h * AD + d4);
+    Qt[(d4 + 0) * AB + r] = v.x; Qt[(d4 + 1) * AB + r] = v.y;
+    Qt[(d4 + 2) * AB + r] = v.z; Qt[(d4 + 3) * AB + r] = v.w;
+  }
+  if (t < AB) { mrow[t] = -INFINITY; lrow[t] = 0.f; }
+  f32x16_t o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+
+  for (int k0 = 0; k0 < T; k0 += AB) {
+    __syncthreads();
+    for (int i = t; i < AB * AD / 4; i += 256) {
+      const int r = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+      if (k0 + r < T) {
+        kv = *(const float4*)(qkv + (size_t)(k0 + r) * ld + W + h * AD + d4);
+        vv = *(const float4*)(qkv + (size_t)(k0 + r) * ld + 2 * W + h * AD + d4);
+      }
+      Kt[(d4 + 0) * AB + r] = kv.x; Kt[(d4 + 1) * AB + r] = kv.y;
+      Kt[(d4 + 2) * AB + r] = kv.z; Kt[(d4 + 3) * AB + r] = kv.w;
+      *(float4*)(Vs + r * AD + d4) = vv;
+    }
+    __syncthreads();
+    // S quadrant = Q[wm] . K[wn]^T
+    f32x16_t sacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll 8
+    for (int kk = 0; kk < AD / 2; ++kk) {
+      const int d = 2 * kk + (lane >> 5);
+      const float a = Qt[d * AB + wm * 32 + (lane & 31)];
+      const float b = Kt[d * AB + wn * 32 + (lane & 31)];
+      sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, sacc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int j = wn * 32 + (lane & 31);
+      Ss[i * ALS + j] = (k0 + j < T) ? sacc[r] * scale : -INFINITY;
+    }
+    __syncthreads();
+    // online softmax: 4 threads per row, 16 columns each
+    {
+      const int i = t >> 2, qd = t & 3;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) mx = fmaxf(mx, Ss[i * ALS + qd * 16 + j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+      const float mold = mrow[i];
+      const float mnew = fmaxf(mold, mx);
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float p = expf(Ss[i * ALS + qd * 16 + j] - mnew);
+        Pt[(qd * 16 + j) * AB + i] = p;
+        ps += p;
+      }
+      ps += __shfl_xor(ps, 1, 64);
+      ps += __shfl_xor(ps, 2, 64);
+      __syncthreads();  // everyone has read mrow[i] before it is updated
+      if (qd == 0) {
+        const float alpha = expf(mold - mnew);
+        arow[i] = alpha;
+        lrow[i] = lrow[i] * alpha + ps;
+        mrow[i] = mnew;
+      }
+    }
+    __syncthreads();
+    // O quadrant (rows wm, dims wn) = alpha * O + P . V
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] *= arow[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+#pragma unroll 8
+    for (int kk = 0; kk < AB / 2; ++kk) {
+      const int k = 2 * kk + (lane >> 5);
+      const float a = Pt[k * AB + wm * 32 + (lane & 31)];
+      const float b = Vs[k * AD + wn * 32 + (lane & 31)];
+      o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, o, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int d = wn * 32 + (lane & 31);
+    if (q0 + i < T) out[(size_t)(q0 + i) * W + h * AD + d] = o[r] / lrow[i];
+  }
+}
+
+void launch_codec_attention(const float* qkv, int T, int heads, int hd, float* out, hipStream_t s) {
+  const size_t lds = (size_t)(3 * AB * AD + AB * ALS + AB * AB + 3 * AB) * sizeof(float);
+  dim3 grid((T + AB - 1) / AB, heads);
+  hipLaunchKernelGGL(codec_attn_kernel, grid, dim3(256), lds, s, qkv, T, heads, out);
+}
+
+// ConvTranspose1d(stride u, padding pad) from Z[t][j*Cout + co] = sum_ci x[t][ci] W[ci][co][j]:
+// output t' receives tap j from input t with t*u - pad + j = t'.
+__global__ void convt_gather_kernel(const float* __restrict__ Z, int T, int Cout, int k, int u,
+                                    int pad, const float* __restrict__ bias, float* __restrict__ y) {
+  const int To = T * u;
+  const long long n = (long long)To * Cout;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int tp = (int)(i / Cout), co = (int)(i % Cout);
+    float acc = bias[co];
+    for (int j = 0; j < k; ++j) {
+      const int num = tp + pad - j;
+      if (num < 0 || num % u) continue;
+      const int ti = num / u;
+      if (ti >= T) continue;
+      acc += Z[(size_t)ti * k * Cout + j * Cout + co];
+    }
+    y[i] = acc;
+  }
+}
+
+void launch_convt_gather(const float* Z, int T, int Cout, int k, int u, int pad,
+                         const float* bias, float* y, hipStream_t s) {
+  const long long n = (long long)T * u * Cout;
+  int grid = (int)std::min<long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(convt_gather_kernel, dim3(grid), dim3(256), 0, s, Z, T, Cout, k, u, pad,
+                     bias, y);
+}
+
+// ISTFTHead (decoder_modules.py:134-147): mag = clip(exp(x[:nb]), max=1e2), p = x[nb:2nb],
+// spec = [mag*cos(p) | mag*sin(p) | 0-pad]
+__global__ void istft_spec_kernel(const float* __restrict__ head, int nb, int ld,
+                                  float* __restrict__ spec) {
+  const int f = blockIdx.x;
+  const float* hr = head + (size_t)f * ld;
+  float* sr = spec + (size_t)f * ld;
+  for (int k = threadIdx.x; k < ld; k += blockDim.x) {
+    if (k < nb) {
+      const float mag = fminf(expf(hr[k]), 1e2f);
+      const float p = hr[nb + k];
+      sr[k] = mag * cosf(p);
+      sr[nb + k] = mag * sinf(p);
+    } else if (k >= 2 * nb) {
+      sr[k] = 0.f;
+    }
+  }
+}
+
+void launch_istft_spec(const float* head, int F, int nb, int ld, float* spec, hipStream_t s) {
+  hipLaunchKernelGGL(istft_spec_kernel, dim3(F), dim3(256), 0, s, head, nb, ld, spec);
+}
+
+// ISTFT 'same' overlap-add (decoder_modules.py:64-93): frames are already irfft'ed and
+// windowed; y[i] = sum_f frames[f][i+pad-f*hop] / sum_f window^2[i+pad-f*hop].
+__global__ void ola_kernel(const float* __restrict__ frames, int F, int nfft, int hop,
+                           const float* __restrict__ win, float* __restrict__ y) {
+  const int pad = (nfft - hop) / 2;
+  const long long L = (long long)F * hop;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < L;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long g = i + pad;
+    long long f_hi = g / hop;
+    if (f_hi > F - 1) f_hi = F - 1;
+    long long f_lo = (g - nfft + hop) / hop;  // smallest f with g - f*hop < nfft
+    if (g - nfft + hop < 0) f_lo = 0;
+    if (f_lo < 0) f_lo = 0;
+    float acc = 0.f, env = 0.f;
+    for (long long f = f_lo; f <= f_hi; ++f) {
+      const int n = (int)(g - f * hop);
+      if (n < 0 || n >= nfft) continue;
+      acc += frames[(size_t)f * nfft + n];
+      env += win[n] * win[n];
+    }
+    y[i] = acc / env;
+  }
+}
+
+void launch_ola(const float* frames, int F, int nfft, int hop, const float* window, float* y,
+                hipStream_t s) {
+  const long long L = (long long)F * hop;
+  int grid = (int)std::min<long long>((L + 255) / 256, 8192);
+  hipLaunchKernelGGL(ola_kernel, dim3(grid), dim3(256), 0, s, frames, F, nfft, hop, window, y);
+}
+
+__global__ void zero_kernel(float* p, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+
+void launch_zero(float* p, long long n, hipStream_t s) {
+  if (n <= 0) return;
+  int grid = (int)std::min<long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(256), 0, s, p, n);
+}
+
+}  // namespace tts

@@ -1,0 +1,137 @@
+// engine.h — the engine object behind the C ABI (one GPU, one stream, owned buffers).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tts_mi355x.h"
+#include "lm_kernels.h"
+
+namespace tts {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                    \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw ::tts::Error(TTS_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e) +    \
+                                        " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")"); \
+  } while (0)
+#define TTS_REQUIRE(cond, msg)                                    \
+  do {                                                            \
+    if (!(cond)) throw ::tts::Error(TTS_E_INVALID, std::string(msg)); \
+  } while (0)
+
+// Device allocation owned by the engine.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void alloc(size_t n) {
+    release();
+    if (n == 0) n = 16;
+    if (hipMalloc(&p, n) != hipSuccess) {
+      p = nullptr;
+      throw Error(TTS_E_OOM, "hipMalloc failed for " + std::to_string(n) + " bytes");
+    }
+    bytes = n;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+  ~DevBuf() { release(); }
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+};
+
+struct LmLayer {
+  bf16_t* ln1;   // [hidden]
+  bf16_t* ln2;
+  bf16_t* wqkv;  // tiled [(H+2KVH)*D][hidden]
+  bf16_t* wo;    // tiled [hidden][H*D]
+  bf16_t* wgu;   // tiled, gate/up n-tiles interleaved [2*ffn][hidden]
+  bf16_t* wd;    // tiled [hidden][ffn]
+};
+
+struct LmModel {
+  tts_lm_config cfg{};
+  bool loaded = false;
+  DevBuf weights;       // one slab for every tiled matrix + norms
+  DevBuf embed_rows;    // row-major embedding [V][hidden] (token gather)
+  DevBuf rope;          // cos | sin  [max_seq][D] bf16 each
+  std::vector<LmLayer> layers;
+  bf16_t* final_norm = nullptr;
+  bf16_t* lm_head = nullptr;  // tiled [V][hidden]
+  std::vector<int> id_to_code;  // host LUT (optional)
+  int qkv_n() const { return (cfg.num_heads + 2 * cfg.num_kv_heads) * cfg.head_dim; }
+};
+
+struct LmWork {
+  int cap_rows = 0;    // activation rows (prefill rows and decode batch)
+  int cap_batch = 0;
+  int cap_seq = 0;
+  DevBuf kv;           // [L][2][slots][KVH][max_seq][D]
+  DevBuf x, xn, qkv, attn_out, act, q_rot, last_x;  // activations
+  DevBuf part_o, part_ml;                           // attention split partials
+  DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
+  DevBuf logits;                                    // scoring output (bf16)
+  DevBuf row_slot, row_pos, row_idx;                // prefill row descriptors
+  DevBuf st_int;                                    // step-state ints
+  DevBuf seen;                                      // [B][V/32]
+  DevBuf out_ids;                                   // [B][max_new]
+  int out_cap = 0;
+  int nsplit_decode = 0, split_decode = 0;
+  int nsplit_prefill = 0, split_prefill = 0;
+  hipGraphExec_t graph = nullptr;
+  int graph_batch = -1;  // the captured step bakes in B, penalty, eos and min_new
+  float graph_pen = -1.f;
+  int graph_eos = -2, graph_min_new = -1;
+  int* h_active = nullptr;  // pinned host copy of n_active (ring of 2)
+};
+
+struct Codec;  // codec_engine.cpp
+
+struct Engine {
+  int device = 0;
+  int num_cu = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {};
+  LmModel lm;
+  LmWork w;
+  Codec* codec = nullptr;
+  float t_prefill_ms = 0.f, t_decode_ms = 0.f;
+  int decode_steps = 0;
+  ~Engine();
+};
+
+hipStream_t pick_stream(Engine* e, void* s);
+void lm_load(Engine* e, const tts_lm_config* cfg, const tts_tensor_desc* t, int n);
+void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens,
+                 int B, int32_t* out_ids, int out_stride, int32_t* out_lens, hipStream_t s);
+void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
+              float* logits, hipStream_t s);
+void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
+                     double* bytes);
+
+// upload a named tensor to device memory as bf16 (convert from f32 if needed)
+void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging);
+void upload_f32(const tts_tensor_desc& d, float* dst, hipStream_t s, DevBuf& staging);
+int64_t numel(const tts_tensor_desc& d);
+
+void codec_load(Engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t, int n);
+void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, float* wav,
+                  int wav_is_device, int64_t* wav_lens, hipStream_t s);
+int codec_samples_per_code(Engine* e);
+void codec_destroy(Codec* c);
+
+}  // namespace tts

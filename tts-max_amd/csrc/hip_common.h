@@ -1,0 +1,66 @@
+// hip_common.h — shared device helpers for the gfx950 kernels (wave64, bf16 bit tricks).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // raw bf16 bits; all arithmetic is done in fp32
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+#define TTS_DEV __device__ __forceinline__
+
+// bf16 -> fp32 is exact: the bf16 bits are the top half of the fp32 pattern.
+TTS_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+TTS_DEV float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+TTS_DEV float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// fp32 -> bf16 round-to-nearest-even, NaN preserved (same rounding as torch's .to(bfloat16)).
+TTS_DEV bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+// Round an fp32 value to the nearest bf16 value, returned as fp32 (torch bf16 op semantics:
+// every bf16 elementwise op computes in fp32 and rounds its result once).
+TTS_DEV float rbf(float f) { return bf2f(f2bf(f)); }
+TTS_DEV uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+TTS_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TTS_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024).  `red` is >= 16 floats of LDS.
+TTS_DEV float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];  // fixed order: deterministic
+  return t;
+}
+TTS_DEV float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+TTS_DEV float silu_f(float x) { return x / (1.0f + expf(-x)); }

@@ -1,0 +1,632 @@
+// lm_engine.cpp — SpeechLM host runtime: weight loading/re-layout, workspaces, chunked
+// prefill, hipGraph-captured decode step, device-side stop bookkeeping.
+//
+// Replaces the reference AR loop `_generate_speech_tokens` -> HF `model.generate`
+// (tts/inference/inferencing.py:94-107; transformers generation/utils.py:2783-2950):
+//   * prefill over the prompt, then one decode step per generated code;
+//   * greedy: argmax over fp32(bf16 logits) after repetition penalty and min-new-tokens EOS
+//     mask; stop at EOS (included in the output) or at max_length (total length);
+//   * batch > 1 = independent sequences (each identical to its batch-1 generate).
+// HF syncs the host every token (`unfinished_sequences.max() == 0`); here the step is one
+// hipGraph replay and the host polls a device counter of active sequences every
+// kPollEvery steps, one poll behind, so the GPU never waits for the host.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "engine.h"
+
+namespace tts {
+
+static constexpr int kPollEvery = 8;
+static constexpr int kPrefillChunk = 64;   // rows per GEMM launch (MFMA A-tiles of 16)
+static constexpr int kMaxPrefillRows = 8192;
+
+int64_t numel(const tts_tensor_desc& d) {
+  int64_t n = 1;
+  for (int i = 0; i < d.ndim; ++i) n *= d.shape[i];
+  return n;
+}
+
+static size_t dtype_size(int dt) {
+  switch (dt) {
+    case TTS_DT_F32: return 4;
+    case TTS_DT_BF16: return 2;
+    case TTS_DT_F16: return 2;
+    case TTS_DT_I32: return 4;
+    case TTS_DT_I64: return 8;
+  }
+  return 0;
+}
+
+void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging) {
+  const int64_t n = numel(d);
+  if (d.dtype == TTS_DT_BF16) {
+    HIP_CHECK(hipMemcpyAsync(dst, d.data, n * 2, d.on_device ? hipMemcpyDeviceToDevice
+                                                             : hipMemcpyHostToDevice, s));
+  } else if (d.dtype == TTS_DT_F32) {
+    const float* src = (const float*)d.data;
+    if (!d.on_device) {
+      if (staging.bytes < (size_t)n * 4) staging.alloc((size_t)n * 4);
+      HIP_CHECK(hipMemcpyAsync(staging.p, d.data, n * 4, hipMemcpyHostToDevice, s));
+      src = staging.as<float>();
+    }
+    launch_f32_to_bf16(src, dst, n, s);
+  } else {
+    throw Error(TTS_E_UNSUPPORTED, std::string("tensor ") + d.name + ": dtype must be bf16 or f32");
+  }
+}
+
+void upload_f32(const tts_tensor_desc& d, float* dst, hipStream_t s, DevBuf&) {
+  TTS_REQUIRE(d.dtype == TTS_DT_F32, std::string("tensor ") + d.name + " must be f32");
+  HIP_CHECK(hipMemcpyAsync(dst, d.data, numel(d) * 4,
+                           d.on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+}
+
+// ------------------------------------------------------------------------ loading -----
+namespace {
+struct TensorMap {
+  std::map<std::string, const tts_tensor_desc*> m;
+  const tts_tensor_desc& get(const std::string& name, std::initializer_list<int64_t> shape) const {
+    auto it = m.find(name);
+    if (it == m.end()) throw Error(TTS_E_INVALID, "missing tensor: " + name);
+    const tts_tensor_desc& d = *it->second;
+    int i = 0;
+    bool ok = (int)shape.size() == d.ndim;
+    for (int64_t v : shape) { if (ok && d.shape[i] != v) ok = false; ++i; }
+    if (!ok) throw Error(TTS_E_INVALID, "bad shape for tensor: " + name);
+    return d;
+  }
+  bool has(const std::string& n) const { return m.count(n) != 0; }
+};
+
+// RoPE table as LlamaRotaryEmbedding computes it (modeling_llama.py:~100-128 and
+// modeling_rope_utils.py:580-660 for llama3), evaluated in double then rounded; the Python
+// host normally passes the torch-computed table instead ("rope.cos"/"rope.sin").
+void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::vector<bf16_t>& sn) {
+  const int D = c.head_dim, S = c.max_seq_len;
+  std::vector<float> inv(D / 2);
+  for (int i = 0; i < D / 2; ++i) {
+    float e = (float)(2 * i) / (float)D;
+    inv[i] = 1.0f / powf(c.rope_theta, e);
+  }
+  if (c.rope_llama3) {
+    const double lo_wl = c.rope_original_max_position / c.rope_low_freq_factor;
+    const double hi_wl = c.rope_original_max_position / c.rope_high_freq_factor;
+    for (int i = 0; i < D / 2; ++i) {
+      const float f = inv[i];
+      const double wl = 2 * M_PI / f;
+      float v = (wl > lo_wl) ? f / c.rope_factor : f;
+      if (!(wl < hi_wl) && !(wl > lo_wl)) {
+        const float sm = (float)((c.rope_original_max_position / wl - c.rope_low_freq_factor) /
+                                 (c.rope_high_freq_factor - c.rope_low_freq_factor));
+        v = (1 - sm) * v / c.rope_factor + sm * v;
+      }
+      inv[i] = v;
+    }
+  }
+  auto to_bf = [](float f) -> bf16_t {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+  };
+  cs.resize((size_t)S * D);
+  sn.resize((size_t)S * D);
+  for (int p = 0; p < S; ++p)
+    for (int i = 0; i < D; ++i) {
+      const float fr = (float)p * inv[i % (D / 2)];
+      cs[(size_t)p * D + i] = to_bf((float)cos((double)fr));
+      sn[(size_t)p * D + i] = to_bf((float)sin((double)fr));
+    }
+}
+}  // namespace
+
+void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int n) {
+  TTS_REQUIRE(cfgp != nullptr, "null config");
+  const tts_lm_config c = *cfgp;
+  TTS_REQUIRE(c.head_dim == 64 || c.head_dim == 128, "head_dim must be 64 or 128");
+  TTS_REQUIRE(c.num_heads == 4 * c.num_kv_heads, "GQA group must be 4 (num_heads == 4*num_kv_heads)");
+  TTS_REQUIRE(c.hidden_size % 256 == 0 && c.intermediate_size % 256 == 0 &&
+                  (c.num_heads * c.head_dim) % 256 == 0,
+              "hidden/intermediate/attention widths must be multiples of 256");
+  TTS_REQUIRE(c.vocab_size % 16 == 0, "vocab_size must be a multiple of 16");
+  TTS_REQUIRE(c.max_batch >= 1 && c.max_batch <= 64, "max_batch must be in [1, 64]");
+  TTS_REQUIRE(c.max_seq_len >= 16, "max_seq_len too small");
+  TensorMap tm;
+  for (int i = 0; i < n; ++i) tm.m[t[i].name] = &t[i];
+  hipStream_t s = e->stream;
+  LmModel& M = e->lm;
+  M.loaded = false;
+  M.cfg = c;
+  const int H = c.num_heads, KVH = c.num_kv_heads, D = c.head_dim, HID = c.hidden_size;
+  const int FF = c.intermediate_size, V = c.vocab_size, L = c.num_layers;
+  const int QKV = M.qkv_n();
+
+  // ---- one slab for everything
+  const size_t per_layer = 2 * (size_t)HID + (size_t)QKV * HID + (size_t)HID * H * D +
+                           2 * (size_t)FF * HID + (size_t)HID * FF;
+  const size_t total = per_layer * L + HID + (size_t)V * HID;
+  M.weights.alloc(total * 2);
+  bf16_t* p = M.weights.as<bf16_t>();
+  M.layers.resize(L);
+  for (int l = 0; l < L; ++l) {
+    LmLayer& ly = M.layers[l];
+    ly.ln1 = p; p += HID;
+    ly.ln2 = p; p += HID;
+    ly.wqkv = p; p += (size_t)QKV * HID;
+    ly.wo = p; p += (size_t)HID * H * D;
+    ly.wgu = p; p += 2 * (size_t)FF * HID;
+    ly.wd = p; p += (size_t)HID * FF;
+  }
+  M.final_norm = p; p += HID;
+  M.lm_head = p; p += (size_t)V * HID;
+
+  DevBuf staging, staging32;
+  staging.alloc((size_t)std::max<size_t>((size_t)V * HID, (size_t)FF * HID) * 2);
+  auto retiled = [&](const tts_tensor_desc& d, bf16_t* dst, int N, int K, int mult, int off) {
+    upload_bf16(d, staging.as<bf16_t>(), s, staging32);
+    launch_retile(staging.as<bf16_t>(), dst, N, K, s, mult, off);
+    HIP_CHECK(hipGetLastError());
+  };
+  const int KT_h = HID / 32;
+  for (int l = 0; l < L; ++l) {
+    LmLayer& ly = M.layers[l];
+    const std::string pre = "model.layers." + std::to_string(l) + ".";
+    upload_bf16(tm.get(pre + "input_layernorm.weight", {HID}), ly.ln1, s, staging32);
+    upload_bf16(tm.get(pre + "post_attention_layernorm.weight", {HID}), ly.ln2, s, staging32);
+    retiled(tm.get(pre + "self_attn.q_proj.weight", {H * D, HID}), ly.wqkv, H * D, HID, 1, 0);
+    retiled(tm.get(pre + "self_attn.k_proj.weight", {KVH * D, HID}),
+            ly.wqkv + (size_t)(H * D / 16) * KT_h * 512, KVH * D, HID, 1, 0);
+    retiled(tm.get(pre + "self_attn.v_proj.weight", {KVH * D, HID}),
+            ly.wqkv + (size_t)((H + KVH) * D / 16) * KT_h * 512, KVH * D, HID, 1, 0);
+    retiled(tm.get(pre + "self_attn.o_proj.weight", {HID, H * D}), ly.wo, HID, H * D, 1, 0);
+    retiled(tm.get(pre + "mlp.gate_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2, 0);
+    retiled(tm.get(pre + "mlp.up_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2, 1);
+    retiled(tm.get(pre + "mlp.down_proj.weight", {HID, FF}), ly.wd, HID, FF, 1, 0);
+  }
+  upload_bf16(tm.get("model.norm.weight", {HID}), M.final_norm, s, staging32);
+  const tts_tensor_desc& emb = tm.get("model.embed_tokens.weight", {V, HID});
+  M.embed_rows.alloc((size_t)V * HID * 2);
+  upload_bf16(emb, M.embed_rows.as<bf16_t>(), s, staging32);
+  if (c.tie_word_embeddings) {
+    launch_retile(M.embed_rows.as<bf16_t>(), M.lm_head, V, HID, s, 1, 0);
+  } else {
+    retiled(tm.get("lm_head.weight", {V, HID}), M.lm_head, V, HID, 1, 0);
+  }
+
+  // ---- RoPE table
+  M.rope.alloc((size_t)2 * c.max_seq_len * D * 2);
+  if (tm.has("rope.cos") && tm.has("rope.sin")) {
+    upload_bf16(tm.get("rope.cos", {c.max_seq_len, D}), M.rope.as<bf16_t>(), s, staging32);
+    upload_bf16(tm.get("rope.sin", {c.max_seq_len, D}),
+                M.rope.as<bf16_t>() + (size_t)c.max_seq_len * D, s, staging32);
+  } else {
+    std::vector<bf16_t> cs, sn;
+    compute_rope_table(c, cs, sn);
+    HIP_CHECK(hipMemcpy(M.rope.as<bf16_t>(), cs.data(), cs.size() * 2, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(M.rope.as<bf16_t>() + cs.size(), sn.data(), sn.size() * 2,
+                        hipMemcpyHostToDevice));
+  }
+  M.id_to_code.clear();
+  if (tm.has("vocab.id_to_code")) {
+    const tts_tensor_desc& d = tm.get("vocab.id_to_code", {V});
+    TTS_REQUIRE(d.dtype == TTS_DT_I32 && !d.on_device, "vocab.id_to_code must be host int32");
+    M.id_to_code.assign((const int*)d.data, (const int*)d.data + V);
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+
+  // ---- workspaces
+  LmWork& w = e->w;
+  if (w.graph) { hipGraphExecDestroy(w.graph); w.graph = nullptr; w.graph_batch = -1; }
+  const int B = c.max_batch, S = c.max_seq_len;
+  const int R = std::max(B, std::min(kMaxPrefillRows, B * S));
+  w.cap_rows = R;
+  w.cap_batch = B;
+  w.cap_seq = S;
+  w.kv.alloc((size_t)L * 2 * B * KVH * S * D * 2);
+  w.x.alloc((size_t)R * HID * 2);
+  w.xn.alloc((size_t)R * HID * 2);
+  w.qkv.alloc((size_t)R * QKV * 2);
+  w.attn_out.alloc((size_t)R * H * D * 2);
+  w.q_rot.alloc((size_t)R * H * D * 2);
+  w.act.alloc((size_t)R * FF * 2);
+  w.last_x.alloc((size_t)B * HID * 2);
+  w.split_decode = (B <= 4) ? 64 : 256;
+  w.nsplit_decode = (S + w.split_decode - 1) / w.split_decode;
+  w.split_prefill = 512;  // = the kv block of torch's CPU flash kernel (kv_split_size)
+  w.nsplit_prefill = (S + w.split_prefill - 1) / w.split_prefill;
+  const size_t part_rows =
+      std::max((size_t)R * w.nsplit_prefill, (size_t)B * w.nsplit_decode);
+  w.part_o.alloc(part_rows * H * D * 4);
+  w.part_ml.alloc(part_rows * H * 2 * 4);
+  w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
+  w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
+  w.row_slot.alloc((size_t)R * 4);
+  w.row_pos.alloc((size_t)R * 4);
+  w.row_idx.alloc((size_t)R * 4);
+  w.st_int.alloc((size_t)B * 8 * 4 + 64);
+  w.seen.alloc((size_t)B * (V / 32 + 1) * 4);
+  w.out_cap = S;
+  w.out_ids.alloc((size_t)B * S * 4);
+  if (!w.h_active) HIP_CHECK(hipHostMalloc((void**)&w.h_active, 64, hipHostMallocDefault));
+  M.loaded = true;
+}
+
+// ------------------------------------------------------------------------ compute -----
+namespace {
+
+struct Ctx {
+  Engine* e;
+  hipStream_t s;
+  const tts_lm_config& c;
+  LmModel& M;
+  LmWork& w;
+  Ctx(Engine* e_, hipStream_t s_) : e(e_), s(s_), c(e_->lm.cfg), M(e_->lm), w(e_->w) {}
+
+  int QKV() const { return M.qkv_n(); }
+
+  // out = epi(x . W^T) over M rows (chunked by 64), RMSNorm prologue if normw != nullptr.
+  void gemm(const bf16_t* x, int rows, int K, const bf16_t* W, int N, const bf16_t* normw,
+            bf16_t* out, int ldo, bf16_t* resid, int epi, const WgemmArgs* logit_extra = nullptr) {
+    for (int r0 = 0; r0 < rows; r0 += kPrefillChunk) {
+      const int m = std::min(kPrefillChunk, rows - r0);
+      WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
+      const bf16_t* xin = x + (size_t)r0 * K;
+      bool norm = normw != nullptr;
+      if (norm && !p.a_lds) {  // fused RMSNorm needs the rows in LDS: normalise separately
+        launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
+        xin = w.xn.as<bf16_t>();
+        norm = false;
+      }
+      WgemmArgs a;
+      if (logit_extra) a = *logit_extra;
+      a.x = xin; a.M = m; a.K = K; a.ldx = K;
+      a.w = W; a.N = N;
+      a.normw = normw; a.eps = c.rms_norm_eps;
+      a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
+      a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
+      launch_wgemm(a, p, epi, norm, s);
+    }
+  }
+
+  AttnArgs attn_args(int layer, int rows, const int* slot, const int* pos, bool decode) {
+    AttnArgs a;
+    const int H = c.num_heads, KVH = c.num_kv_heads, D = c.head_dim;
+    const size_t kv_layer = (size_t)c.max_batch * KVH * c.max_seq_len * D;
+    a.qkv = w.qkv.as<bf16_t>(); a.ld_qkv = QKV(); a.rows = rows;
+    a.row_slot = slot; a.row_pos = pos;
+    a.kcache = w.kv.as<bf16_t>() + (size_t)layer * 2 * kv_layer;
+    a.vcache = a.kcache + kv_layer;
+    a.max_seq = c.max_seq_len;
+    a.rope_cos = M.rope.as<bf16_t>();
+    a.rope_sin = a.rope_cos + (size_t)c.max_seq_len * D;
+    a.H = H; a.KVH = KVH; a.D = D;
+    a.scale = (float)(1.0 / sqrt((double)D));
+    a.split = decode ? w.split_decode : w.split_prefill;
+    a.nsplit = decode ? w.nsplit_decode : w.nsplit_prefill;
+    a.part_o = w.part_o.as<float>(); a.part_ml = w.part_ml.as<float>();
+    a.q_rot = w.q_rot.as<bf16_t>(); a.out = w.attn_out.as<bf16_t>();
+    return a;
+  }
+
+  // One transformer stack pass over `rows` rows held in w.x.
+  void layers(int rows, const int* slot, const int* pos, bool decode) {
+    const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
+    for (int l = 0; l < c.num_layers; ++l) {
+      const LmLayer& ly = M.layers[l];
+      gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(),
+           nullptr, EPI_STORE);
+      AttnArgs a = attn_args(l, rows, slot, pos, decode);
+      if (decode) {
+        launch_attn_decode(a, true, s);
+      } else {
+        launch_rope_append(a, s);
+        launch_attn_decode(a, false, s);
+      }
+      launch_attn_combine(a, s);
+      gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
+           w.x.as<bf16_t>(), EPI_RESID);
+      gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
+           EPI_SWIGLU);
+      gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),
+           EPI_RESID);
+    }
+  }
+
+  StepState state(int B, int eos, int min_new) {
+    StepState st;
+    int* base = w.st_int.as<int>();
+    st.tokens = base;
+    st.pos = base + B;
+    st.gen_count = base + 2 * B;
+    st.limit = base + 3 * B;
+    st.done = base + 4 * B;
+    st.eos_mask = base + 5 * B;
+    st.n_active = base + 6 * B;
+    st.seen = w.seen.as<uint32_t>();
+    st.seen_stride = c.vocab_size / 32 + 1;
+    st.out_ids = w.out_ids.as<int>();
+    st.out_stride = w.out_cap;
+    st.eos_id = eos;
+    st.min_new = min_new;
+    return st;
+  }
+
+  // lm_head over B rows of `xin` + greedy finalize (state update, next embedding -> w.x)
+  void head_and_pick(const bf16_t* xin, int B, const StepState& st, float penalty) {
+    WgemmArgs ex;
+    ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = penalty;
+    ex.eos_mask = st.eos_mask;
+    ex.part_val = w.lpart_v.as<float>(); ex.part_idx = w.lpart_i.as<int>();
+    ex.part_stride = LOGITS_MAX_PARTS;
+    TTS_REQUIRE(B <= kPrefillChunk, "batch larger than one GEMM chunk");
+    WgemmPlan p = plan_wgemm(B, c.vocab_size, c.hidden_size, EPI_LOGITS, e->num_cu);
+    gemm(xin, B, c.hidden_size, M.lm_head, c.vocab_size, M.final_norm, nullptr, 0, nullptr,
+         EPI_LOGITS, &ex);
+    launch_finalize_greedy(ex.part_val, ex.part_idx, LOGITS_MAX_PARTS, p.grid, st, B,
+                           M.embed_rows.as<bf16_t>(), w.x.as<bf16_t>(), c.hidden_size, s);
+  }
+};
+
+}  // namespace
+
+static void check_launch() { HIP_CHECK(hipGetLastError()); }
+
+// Prefill a group of sequences [b0, b0+nb): rows = sum of their prompt lengths.
+static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, int B,
+                               std::vector<int>& last_rows, int& rows) {
+  std::vector<int> slot, pos, tok;
+  rows = 0;
+  last_rows.resize(B);
+  for (int b = 0; b < B; ++b) {
+    for (int i = 0; i < lens[b]; ++i) {
+      slot.push_back(b);
+      pos.push_back(i);
+      tok.push_back(ids[rows + i]);
+    }
+    rows += lens[b];
+    last_rows[b] = rows - 1;
+  }
+  TTS_REQUIRE(rows <= X.w.cap_rows, "total prompt rows exceed the prefill workspace");
+  HIP_CHECK(hipMemcpyAsync(X.w.row_slot.p, slot.data(), rows * 4, hipMemcpyHostToDevice, X.s));
+  HIP_CHECK(hipMemcpyAsync(X.w.row_pos.p, pos.data(), rows * 4, hipMemcpyHostToDevice, X.s));
+  HIP_CHECK(hipMemcpyAsync(X.w.row_idx.p, tok.data(), rows * 4, hipMemcpyHostToDevice, X.s));
+  launch_embed(X.w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), X.w.x.as<bf16_t>(), rows,
+               X.c.hidden_size, X.s);
+}
+
+void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens,
+                 int B, int32_t* out_ids, int out_stride, int32_t* out_lens, hipStream_t s) {
+  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
+  TTS_REQUIRE(p != nullptr && ids != nullptr && lens != nullptr, "null argument");
+  TTS_REQUIRE(B >= 1 && B <= e->w.cap_batch, "batch out of range");
+  TTS_REQUIRE(!p->do_sample, "sampling (do_sample=1) is not implemented yet; use greedy");
+  Ctx X(e, s);
+  const tts_lm_config& c = X.c;
+  const int V = c.vocab_size;
+  // ---- host-side state init
+  std::vector<int> st_host(7 * B + 1, 0);
+  std::vector<uint32_t> seen((size_t)B * (V / 32 + 1), 0u);
+  int max_new = 0, off = 0;
+  for (int b = 0; b < B; ++b) {
+    const int P = lens[b];
+    TTS_REQUIRE(P >= 1, "empty prompt");
+    // HF: max_length counts the prompt; input length >= max_length is a ValueError
+    // (generation/utils.py _validate_generated_length)
+    TTS_REQUIRE(P < p->max_length, "input length >= max_length");
+    const int limit = p->max_length - P;
+    TTS_REQUIRE(P + limit <= c.max_seq_len, "prompt + max new tokens exceed max_seq_len");
+    TTS_REQUIRE(limit <= out_stride && limit <= e->w.out_cap, "out_stride too small");
+    for (int i = 0; i < P; ++i) {
+      const int t = ids[off + i];
+      TTS_REQUIRE(t >= 0 && t < V, "token id out of range");
+      seen[(size_t)b * (V / 32 + 1) + (t >> 5)] |= 1u << (t & 31);
+    }
+    off += P;
+    st_host[1 * B + b] = P - 1;  // pos: finalize advances it to P for the first new token
+    st_host[3 * B + b] = limit;
+    st_host[5 * B + b] = (p->min_new_tokens > 0) ? p->eos_token_id : -1;
+    max_new = std::max(max_new, limit);
+  }
+  st_host[6 * B] = B;
+  StepState st = X.state(B, p->eos_token_id, p->min_new_tokens);
+  HIP_CHECK(hipMemcpyAsync(e->w.st_int.p, st_host.data(), st_host.size() * 4,
+                           hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(e->w.seen.p, seen.data(), seen.size() * 4, hipMemcpyHostToDevice, s));
+  // rows' slots are 0..B-1 in the decode phase: prepare a persistent identity map
+  HIP_CHECK(hipEventRecord(e->ev[2], s));
+
+  // ---- prefill
+  std::vector<int> last_rows;
+  int rows = 0;
+  prefill_rows_setup(X, ids, lens, B, last_rows, rows);
+  X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
+  HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, last_rows.data(), B * 4, hipMemcpyHostToDevice, s));
+  launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, e->w.row_idx.as<int>(),
+                     e->w.last_x.as<bf16_t>(), B, c.hidden_size, s);
+  X.head_and_pick(e->w.last_x.as<bf16_t>(), B, st, p->repetition_penalty);
+  check_launch();
+  HIP_CHECK(hipEventRecord(e->ev[3], s));
+
+  // ---- decode: identity slot map; positions live in the step state
+  std::vector<int> ident(B);
+  for (int b = 0; b < B; ++b) ident[b] = b;
+  HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, ident.data(), B * 4, hipMemcpyHostToDevice, s));
+  // (the embedding of each sequence's next token is already in w.x rows 0..B-1)
+  const float pen = p->repetition_penalty;
+  auto step = [&](hipStream_t ss) {
+    Ctx Y(e, ss);
+    Y.layers(B, e->w.row_slot.as<int>(), st.pos, true);
+    Y.head_and_pick(e->w.x.as<bf16_t>(), B, st, pen);
+  };
+  // the graph bakes in B, the penalty and eos/min_new (kernel args): recapture on change
+  LmWork& W = e->w;
+  if (W.graph && (W.graph_batch != B || W.graph_pen != pen || W.graph_eos != p->eos_token_id ||
+                  W.graph_min_new != p->min_new_tokens)) {
+    hipGraphExecDestroy(e->w.graph);
+    e->w.graph = nullptr;
+  }
+  if (!e->w.graph) {
+    hipStream_t cs;
+    HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t g;
+    HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    step(cs);
+    HIP_CHECK(hipStreamEndCapture(cs, &g));
+    HIP_CHECK(hipGraphInstantiate(&e->w.graph, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+    HIP_CHECK(hipStreamDestroy(cs));
+    W.graph_batch = B;
+    W.graph_pen = pen;
+    W.graph_eos = p->eos_token_id;
+    W.graph_min_new = p->min_new_tokens;
+  }
+  int steps = 0;
+  int polls = 0;
+  for (int k = 1; k < max_new; ++k) {
+    HIP_CHECK(hipGraphLaunch(e->w.graph, s));
+    ++steps;
+    if (k % kPollEvery == 0) {
+      const int slot = polls & 1;
+      HIP_CHECK(hipMemcpyAsync(&e->w.h_active[slot], st.n_active, 4, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipEventRecord(e->ev[slot], s));
+      if (polls > 0) {
+        HIP_CHECK(hipEventSynchronize(e->ev[slot ^ 1]));
+        if (e->w.h_active[slot ^ 1] == 0) break;
+      }
+      ++polls;
+    }
+  }
+  HIP_CHECK(hipEventRecord(e->ev[1], s));
+  // ---- results
+  std::vector<int> gc(B);
+  HIP_CHECK(hipMemcpyAsync(gc.data(), st.gen_count, B * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  for (int b = 0; b < B; ++b) {
+    out_lens[b] = gc[b];
+    HIP_CHECK(hipMemcpy(out_ids + (size_t)b * out_stride, st.out_ids + (size_t)b * st.out_stride,
+                        (size_t)gc[b] * 4, hipMemcpyDeviceToHost));
+  }
+  float t0 = 0.f, t1 = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&t0, e->ev[2], e->ev[3]));
+  HIP_CHECK(hipEventElapsedTime(&t1, e->ev[3], e->ev[1]));
+  e->t_prefill_ms = t0;
+  e->t_decode_ms = t1;
+  e->decode_steps = steps;
+}
+
+void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
+                     double* bytes) {
+  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
+  TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
+  TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
+  TTS_REQUIRE(which >= 0 && which <= 5 && iters >= 1, "bad kernel selector");
+  hipStream_t s = e->stream;
+  Ctx X(e, s);
+  const tts_lm_config& c = X.c;
+  const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
+  const int V = c.vocab_size, QKV = X.QKV();
+  std::vector<int> tok(rows), slot(rows), pos(rows, ctx - 1);
+  for (int r = 0; r < rows; ++r) { tok[r] = (r * 7919 + 11) % V; slot[r] = r; }
+  HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, tok.data(), rows * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, slot.data(), rows * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(e->w.row_pos.p, pos.data(), rows * 4, hipMemcpyHostToDevice, s));
+  launch_embed(e->w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), rows, HID, s);
+  const LmLayer& ly = X.M.layers[0];
+  StepState st = X.state(rows, -1, 0);
+  std::vector<int> zeros(7 * rows + 1, 0);
+  for (int r = 0; r < rows; ++r) zeros[5 * rows + r] = -1;  // no EOS mask
+  HIP_CHECK(hipMemcpyAsync(e->w.st_int.p, zeros.data(), zeros.size() * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemsetAsync(e->w.seen.p, 0, (size_t)rows * st.seen_stride * 4, s));
+  // real activations for every stage
+  X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr, EPI_STORE);
+  HIP_CHECK(hipMemsetAsync(e->w.attn_out.p, 0, (size_t)rows * HD * 2, s));
+  HIP_CHECK(hipMemsetAsync(e->w.act.p, 0, (size_t)rows * FF * 2, s));
+  AttnArgs aa = X.attn_args(0, rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
+  WgemmArgs ex;
+  ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = 1.1f; ex.eos_mask = st.eos_mask;
+  ex.part_val = e->w.lpart_v.as<float>(); ex.part_idx = e->w.lpart_i.as<int>();
+  ex.part_stride = LOGITS_MAX_PARTS;
+  double b = 0;
+  const double act_rw = 2.0 * rows;
+  auto launch = [&]() {
+    switch (which) {
+      case 0:
+        X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr, EPI_STORE);
+        b = 2.0 * QKV * HID + act_rw * (HID + QKV) + 2.0 * HID;
+        break;
+      case 1:
+        X.gemm(e->w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID);
+        b = 2.0 * HID * HD + act_rw * (HD + 2 * HID);
+        break;
+      case 2:
+        X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, e->w.act.as<bf16_t>(), FF, nullptr, EPI_SWIGLU);
+        b = 2.0 * 2 * FF * HID + act_rw * (HID + FF) + 2.0 * HID;
+        break;
+      case 3:
+        X.gemm(e->w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID);
+        b = 2.0 * HID * FF + act_rw * (FF + 2 * HID);
+        break;
+      case 4:
+        X.gemm(e->w.x.as<bf16_t>(), rows, HID, X.M.lm_head, V, X.M.final_norm, nullptr, 0, nullptr, EPI_LOGITS, &ex);
+        b = 2.0 * V * HID + act_rw * HID + 2.0 * HID + rows * (V / 8.0);
+        break;
+      case 5:
+        launch_attn_decode(aa, true, s);
+        b = (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2 + act_rw * QKV;
+        break;
+    }
+  };
+  launch();
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(e->ev[2], s));
+  for (int i = 0; i < iters; ++i) launch();
+  HIP_CHECK(hipEventRecord(e->ev[3], s));
+  HIP_CHECK(hipEventSynchronize(e->ev[3]));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+  *avg_ms = ms / iters;
+  *bytes = b;
+}
+
+void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
+              float* logits, hipStream_t s) {
+  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
+  TTS_REQUIRE(B >= 1 && B <= e->w.cap_batch, "batch out of range");
+  Ctx X(e, s);
+  const tts_lm_config& c = X.c;
+  for (int b = 0; b < B; ++b) {
+    TTS_REQUIRE(lens[b] >= n_last && lens[b] <= c.max_seq_len, "bad sequence length");
+  }
+  std::vector<int> last_rows;
+  int rows = 0;
+  prefill_rows_setup(X, ids, lens, B, last_rows, rows);
+  X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
+  // gather the last n_last rows of every sequence
+  std::vector<int> sel;
+  for (int b = 0; b < B; ++b)
+    for (int i = n_last - 1; i >= 0; --i) sel.push_back(last_rows[b] - i);
+  const int nsel = (int)sel.size();
+  DevBuf sel_d, xs, lg;
+  sel_d.alloc(nsel * 4);
+  xs.alloc((size_t)nsel * c.hidden_size * 2);
+  lg.alloc((size_t)nsel * c.vocab_size * 2);
+  HIP_CHECK(hipMemcpyAsync(sel_d.p, sel.data(), nsel * 4, hipMemcpyHostToDevice, s));
+  launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, sel_d.as<int>(), xs.as<bf16_t>(), nsel,
+                     c.hidden_size, s);
+  X.gemm(xs.as<bf16_t>(), nsel, c.hidden_size, X.M.lm_head, c.vocab_size, X.M.final_norm,
+         lg.as<bf16_t>(), c.vocab_size, nullptr, EPI_STORE);
+  check_launch();
+  std::vector<uint16_t> h((size_t)nsel * c.vocab_size);
+  HIP_CHECK(hipMemcpyAsync(h.data(), lg.p, h.size() * 2, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  for (size_t i = 0; i < h.size(); ++i) {
+    uint32_t u = (uint32_t)h[i] << 16;
+    memcpy(&logits[i], &u, 4);
+  }
+}
+
+}  // namespace tts

@@ -1,0 +1,103 @@
+// lm_kernels.h — host-side declarations of the SpeechLM kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace tts {
+
+typedef uint16_t bf16_t;
+
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
+constexpr int LOGITS_MAX_PARTS = 1024;  // lm_head workgroups = argmax partials per row
+
+struct WgemmArgs {
+  const bf16_t* x = nullptr;  // A: [M][ldx] bf16 activations
+  int M = 0, K = 0, ldx = 0;
+  const bf16_t* w = nullptr;  // B: tiled weights (see lm_gemm.hip)
+  int N = 0;
+  const bf16_t* normw = nullptr;  // RMSNorm weight [K] (NORM prologue)
+  float eps = 0.f;
+  bf16_t* out = nullptr;  // [M][ldo]
+  int ldo = 0;
+  bf16_t* resid = nullptr;  // EPI_RESID: residual stream, updated in place
+  // EPI_LOGITS
+  const uint32_t* seen = nullptr;  // [M][seen_stride] bitmap of ids present in the sequence
+  int seen_stride = 0;
+  float penalty = 1.f;
+  const int* eos_mask = nullptr;  // [M] token id forced to -inf (or -1)
+  float* part_val = nullptr;      // [M][part_stride]
+  int* part_idx = nullptr;
+  int part_stride = 0;
+};
+
+struct WgemmPlan {
+  int ksplit = 1;
+  int grid = 1;
+  bool a_lds = true;
+};
+
+// dest n-tile index = nt * nt_mult + nt_off (nt_mult = 2 interleaves gate/up tiles)
+void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, hipStream_t s, int nt_mult = 1,
+                   int nt_off = 0);
+WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu);
+bool wgemm_supported(int M, int N, int K, int epi);
+void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
+
+// ---- elementwise / small kernels (lm_ops.hip)
+void launch_rmsnorm(const bf16_t* x, int ldx, const bf16_t* w, float eps, bf16_t* y, int ldy,
+                    int M, int K, hipStream_t s);
+void launch_embed(const int* tokens, const bf16_t* table, bf16_t* x, int M, int hidden,
+                  hipStream_t s);
+void launch_gather_rows(const bf16_t* x, int ld, const int* rows, bf16_t* y, int M, int hidden,
+                        hipStream_t s);
+void launch_synth_fill(void* dst, int dtype, long long n, unsigned long long seed, float scale,
+                       hipStream_t s);
+void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s);
+
+// ---- attention (lm_attn.hip)
+struct AttnArgs {
+  const bf16_t* qkv = nullptr;  // [rows][ld_qkv]: q (H*D) | k (KVH*D) | v (KVH*D)
+  int ld_qkv = 0;
+  int rows = 0;
+  const int* row_slot = nullptr;  // KV slot (sequence) of each query row
+  const int* row_pos = nullptr;   // absolute position of each query row
+  bf16_t* kcache = nullptr;       // this layer: [slots][KVH][max_seq][D]
+  bf16_t* vcache = nullptr;
+  int max_seq = 0;
+  const bf16_t* rope_cos = nullptr;  // [max_seq][D]
+  const bf16_t* rope_sin = nullptr;
+  int H = 0, KVH = 0, D = 0;
+  float scale = 0.f;
+  int split = 0;      // positions per split-K chunk
+  int nsplit = 0;     // max chunks per row (grid.y)
+  float* part_o = nullptr;  // [rows][H][nsplit][D]
+  float* part_ml = nullptr; // [rows][H][nsplit][2] (running max, sum)
+  bf16_t* q_rot = nullptr;  // prefill: roped q [rows][H*D]
+  bf16_t* out = nullptr;    // [rows][H*D] bf16
+};
+void launch_rope_append(const AttnArgs& a, hipStream_t s);       // prefill: rope q,k; append k,v
+void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
+void launch_attn_combine(const AttnArgs& a, hipStream_t s);
+
+// ---- sampling / bookkeeping (lm_ops.hip)
+struct StepState {
+  int* tokens;        // [B] token fed to the next step
+  int* pos;           // [B] position of the next token (= current length)
+  int* gen_count;     // [B] tokens generated so far
+  int* limit;         // [B] max new tokens
+  int* done;          // [B]
+  int* eos_mask;      // [B] eos id while gen_count < min_new, else -1
+  uint32_t* seen;     // [B][seen_stride]
+  int seen_stride;
+  int* out_ids;       // [B][out_stride]
+  int out_stride;
+  int* n_active;      // [1]
+  int eos_id;
+  int min_new;
+};
+void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
+                            int nparts, StepState st, int B, const bf16_t* embed, bf16_t* x,
+                            int hidden, hipStream_t s);
+
+}  // namespace tts

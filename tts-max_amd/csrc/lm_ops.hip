@@ -1,0 +1,169 @@
+// lm_ops.hip — small SpeechLM kernels: standalone RMSNorm (prefill chunks), token
+// embedding gather, row gather, greedy finalize (argmax reduce + per-sequence bookkeeping),
+// and the deterministic synthetic-weight generator shared with tts_amd/synth.py.
+#include "hip_common.h"
+#include "lm_kernels.h"
+
+namespace tts {
+
+// LlamaRMSNorm (transformers modeling_llama.py:62-67) with bf16 in/out.
+__global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, int ldx, const bf16_t* __restrict__ w,
+                               float eps, bf16_t* __restrict__ y, int ldy, int K) {
+  __shared__ float red[16];
+  const bf16_t* xr = x + (size_t)blockIdx.x * ldx;
+  bf16_t* yr = y + (size_t)blockIdx.x * ldy;
+  float ss = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
+    const u32x4_t v = *(const u32x4_t*)(xr + k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = bf_lo(v[q]), hi = bf_hi(v[q]);
+      ss += lo * lo + hi * hi;
+    }
+  }
+  ss = block_sum(ss, red);
+  const float r = 1.0f / sqrtf(ss / (float)K + eps);
+  for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
+    u32x4_t v = *(const u32x4_t*)(xr + k);
+    const u32x4_t g = *(const u32x4_t*)(w + k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+    *(u32x4_t*)(yr + k) = v;
+  }
+}
+
+void launch_rmsnorm(const bf16_t* x, int ldx, const bf16_t* w, float eps, bf16_t* y, int ldy,
+                    int M, int K, hipStream_t s) {
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
+}
+
+__global__ void embed_kernel(const int* __restrict__ tokens, const bf16_t* __restrict__ table,
+                             bf16_t* __restrict__ x, int hidden) {
+  const int t = tokens[blockIdx.x];
+  const u32x4_t* src = (const u32x4_t*)(table + (size_t)t * hidden);
+  u32x4_t* dst = (u32x4_t*)(x + (size_t)blockIdx.x * hidden);
+  for (int i = threadIdx.x; i < hidden / 8; i += blockDim.x) dst[i] = src[i];
+}
+
+void launch_embed(const int* tokens, const bf16_t* table, bf16_t* x, int M, int hidden,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, s, tokens, table, x, hidden);
+}
+
+__global__ void gather_rows_kernel(const bf16_t* __restrict__ x, int ld, const int* __restrict__ rows,
+                                   bf16_t* __restrict__ y, int hidden) {
+  const u32x4_t* src = (const u32x4_t*)(x + (size_t)rows[blockIdx.x] * ld);
+  u32x4_t* dst = (u32x4_t*)(y + (size_t)blockIdx.x * hidden);
+  for (int i = threadIdx.x; i < hidden / 8; i += blockDim.x) dst[i] = src[i];
+}
+
+void launch_gather_rows(const bf16_t* x, int ld, const int* rows, bf16_t* y, int M, int hidden,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(M), dim3(256), 0, s, x, ld, rows, y, hidden);
+}
+
+// --------------------------------------------------------------- greedy finalize -------
+// One workgroup per sequence: reduce the lm_head partial argmaxes (lowest index on ties),
+// append the token, update the repetition-penalty id set, stop on EOS / length, and gather
+// the next step's input embedding.
+__global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                       int part_stride, int nparts, StepState st,
+                                       const bf16_t* __restrict__ embed, bf16_t* __restrict__ x,
+                                       int hidden) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ int stok;
+  const int b = blockIdx.x;
+  if (st.done[b]) return;
+  float v = -INFINITY;
+  int i = 0x7fffffff;
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
+    const float v2 = pv[(size_t)b * part_stride + p];
+    const int i2 = pi[(size_t)b * part_stride + p];
+    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(v, o, 64);
+    const int i2 = __shfl_xor(i, o, 64);
+    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+  }
+  if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; si[threadIdx.x >> 6] = i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      if (sv[w] > v || (sv[w] == v && si[w] < i)) { v = sv[w]; i = si[w]; }
+    // all-(-inf) rows cannot happen (only EOS is masked); guard anyway
+    const int tok = (i == 0x7fffffff) ? 0 : i;
+    const int g = st.gen_count[b];
+    st.out_ids[(size_t)b * st.out_stride + g] = tok;
+    st.gen_count[b] = g + 1;
+    st.seen[(size_t)b * st.seen_stride + (tok >> 5)] |= 1u << (tok & 31);
+    st.tokens[b] = tok;
+    st.pos[b] += 1;
+    const bool stop = (tok == st.eos_id) || (g + 1 >= st.limit[b]);
+    st.eos_mask[b] = (g + 1 < st.min_new) ? st.eos_id : -1;
+    if (stop) {
+      st.done[b] = 1;
+      atomicSub(st.n_active, 1);
+    }
+    stok = tok;
+  }
+  __syncthreads();
+  const u32x4_t* src = (const u32x4_t*)(embed + (size_t)stok * hidden);
+  u32x4_t* dst = (u32x4_t*)(x + (size_t)b * hidden);
+  for (int k = threadIdx.x; k < hidden / 8; k += blockDim.x) dst[k] = src[k];
+}
+
+void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
+                            int nparts, StepState st, int B, const bf16_t* embed, bf16_t* x,
+                            int hidden, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_greedy_kernel, dim3(B), dim3(256), 0, s, part_val, part_idx,
+                     part_stride, nparts, st, embed, x, hidden);
+}
+
+// --------------------------------------------------------------- synthetic weights -----
+// Counter-based generator (splitmix64 of seed + index): value = (2u - 1) * scale with
+// u = top 24 bits / 2^24.  Bit-identical to tts_amd/synth.py (numpy), so the GPU box can
+// regenerate the exact weights the golden fixtures were produced with.
+TTS_DEV float synth_value(unsigned long long seed, unsigned long long idx, float scale) {
+  unsigned long long z = seed + (idx + 1ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  const float u = (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
+  const float t = __fsub_rn(__fmul_rn(u, 2.0f), 1.0f);
+  return __fmul_rn(t, scale);
+}
+
+__global__ void synth_fill_kernel(void* dst, int dtype, long long n, unsigned long long seed,
+                                  float scale) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float v = synth_value(seed, (unsigned long long)i, scale);
+    if (dtype == 0) ((float*)dst)[i] = v;
+    else ((bf16_t*)dst)[i] = f2bf(v);
+  }
+}
+
+void launch_synth_fill(void* dst, int dtype, long long n, unsigned long long seed, float scale,
+                       hipStream_t s) {
+  long long g = (n + 255) / 256;
+  int grid = (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+  hipLaunchKernelGGL(synth_fill_kernel, dim3(grid), dim3(256), 0, s, dst, dtype, n, seed, scale);
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s) {
+  long long g = (n + 255) / 256;
+  int grid = (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid), dim3(256), 0, s, x, y, n);
+}
+
+}  // namespace tts

@@ -1,0 +1,212 @@
+"""Deterministic synthetic weights and inputs (no checkpoints are reachable offline).
+
+``synth_values`` is bit-identical to the device generator ``tts_synth_fill``
+(csrc/lm_ops.hip): value_i = (2*u_i - 1) * scale with u_i the top 24 bits of
+splitmix64(seed + (i+1)*0x9E3779B97F4A7C15) / 2^24.  The GPU box can therefore rebuild,
+on the device and in milliseconds, exactly the weights the golden fixtures were produced
+with on the CPU.
+
+Weight names are the reference state-dict keys: HF Llama keys for the SpeechLM and the
+``Decoder`` keys of tts/core/codec/decoder.py for the codec.
+"""
+
+from __future__ import annotations
+
+import math
+import zlib
+
+import numpy as np
+import torch
+
+from . import configs
+
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def tensor_seed(base_seed: int, name: str) -> int:
+    return (base_seed * 0x100000001B3 + zlib.crc32(name.encode())) & 0xFFFFFFFFFFFFFFFF
+
+
+def synth_values(seed: int, n: int, scale: float, chunk: int = 1 << 24) -> np.ndarray:
+    """float32 array of n synthetic values (see module docstring)."""
+    out = np.empty(n, dtype=np.float32)
+    s = np.uint64(seed)
+    sc = np.float32(scale)
+    with np.errstate(over="ignore"):
+        for a in range(0, n, chunk):
+            b = min(n, a + chunk)
+            z = s + (np.arange(a + 1, b + 1, dtype=np.uint64) * _GOLD)
+            z = (z ^ (z >> np.uint64(30))) * _M1
+            z = (z ^ (z >> np.uint64(27))) * _M2
+            z = z ^ (z >> np.uint64(31))
+            u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+            out[a:b] = (u * np.float32(2.0) - np.float32(1.0)) * sc
+    return out
+
+
+# ------------------------------------------------------------------ SpeechLM weights ---
+
+def lm_tensor_specs(arch: configs.LmArch) -> list[tuple[str, tuple[int, ...], float, float]]:
+    """(name, shape, scale, offset) for every LlamaForCausalLM tensor.  value = offset + synth.
+
+    Linear weights: uniform with std 0.02 (scale 0.02*sqrt(3)); norm weights 1 +- 0.2 so the
+    bf16 `weight * x` step is exercised; the (tied) embedding uses std 0.08 which widens the
+    greedy argmax margins ("lm_head scaled x4")."""
+    H, KVH, D, HID, FF = arch.num_heads, arch.num_kv_heads, arch.head_dim, arch.hidden_size, arch.intermediate_size
+    lin = 0.02 * math.sqrt(3.0)
+    specs = [("model.embed_tokens.weight", (arch.vocab_size, HID), 0.08 * math.sqrt(3.0), 0.0)]
+    for i in range(arch.num_layers):
+        p = f"model.layers.{i}."
+        specs += [
+            (p + "input_layernorm.weight", (HID,), 0.2, 1.0),
+            (p + "self_attn.q_proj.weight", (H * D, HID), lin, 0.0),
+            (p + "self_attn.k_proj.weight", (KVH * D, HID), lin, 0.0),
+            (p + "self_attn.v_proj.weight", (KVH * D, HID), lin, 0.0),
+            (p + "self_attn.o_proj.weight", (HID, H * D), lin, 0.0),
+            (p + "post_attention_layernorm.weight", (HID,), 0.2, 1.0),
+            (p + "mlp.gate_proj.weight", (FF, HID), lin, 0.0),
+            (p + "mlp.up_proj.weight", (FF, HID), lin, 0.0),
+            (p + "mlp.down_proj.weight", (HID, FF), lin, 0.0),
+        ]
+    specs.append(("model.norm.weight", (HID,), 0.2, 1.0))
+    if not arch.tie_word_embeddings:
+        specs.append(("lm_head.weight", (arch.vocab_size, HID), 0.08 * math.sqrt(3.0), 0.0))
+    return specs
+
+
+def lm_weights_cpu(arch: configs.LmArch, seed: int) -> dict[str, torch.Tensor]:
+    """bf16 CPU tensors (numpy generator)."""
+    out = {}
+    for name, shape, scale, off in lm_tensor_specs(arch):
+        n = int(np.prod(shape))
+        v = synth_values(tensor_seed(seed, name), n, scale)
+        t = torch.from_numpy(v).reshape(shape)
+        if off:
+            t = t + off  # fp32 add, then one RNE rounding to bf16 (same on device)
+        out[name] = t.to(torch.bfloat16)
+    return out
+
+
+def lm_weights_device(arch: configs.LmArch, seed: int, device) -> dict[str, torch.Tensor]:
+    """Same values generated on the GPU by tts_synth_fill (bit-identical to lm_weights_cpu)."""
+    from . import _lib
+
+    lib = _lib.load_library()
+    out = {}
+    for name, shape, scale, off in lm_tensor_specs(arch):
+        n = int(np.prod(shape))
+        if off:
+            t = torch.empty(shape, dtype=torch.float32, device=device)
+            _lib.check(lib.tts_synth_fill(t.data_ptr(), _lib.DT_F32, n, tensor_seed(seed, name), scale,
+                                          _lib.stream_ptr()))
+            out[name] = (t + off).to(torch.bfloat16)
+        else:
+            t = torch.empty(shape, dtype=torch.bfloat16, device=device)
+            _lib.check(lib.tts_synth_fill(t.data_ptr(), _lib.DT_BF16, n, tensor_seed(seed, name), scale,
+                                          _lib.stream_ptr()))
+            out[name] = t
+    torch.cuda.synchronize()
+    return out
+
+
+# ---------------------------------------------------------------------- codec weights ---
+
+def codec_tensor_specs(cfg: configs.CodecArch) -> list[tuple[str, tuple[int, ...], float, float]]:
+    """(name, shape, scale, offset) for the reference Decoder state dict (decoder.py:14-67)."""
+    D, VQ = cfg.hidden_dim, cfg.vq_dim
+    w = 0.02 * math.sqrt(3.0)
+    b = 0.01
+    specs = [
+        ("decoder.quantizer.project_out.weight", (VQ, 8), 1.0 / math.sqrt(8), 0.0),
+        ("decoder.quantizer.project_out.bias", (VQ,), b, 0.0),
+        ("fc_post_a.weight", (D, VQ), 1.0 / math.sqrt(VQ), 0.0),
+        ("fc_post_a.bias", (D,), b, 0.0),
+        ("decoder.backbone.embed.weight", (D, D, 7), w, 0.0),
+        ("decoder.backbone.embed.bias", (D,), b, 0.0),
+    ]
+
+    def resblock(pre, C, temb=False):
+        s = [
+            (pre + "norm1.weight", (C,), 0.1, 1.0), (pre + "norm1.bias", (C,), 0.05, 0.0),
+            (pre + "conv1.weight", (C, C, 3), w, 0.0), (pre + "conv1.bias", (C,), b, 0.0),
+        ]
+        if temb:  # exists in upsampler blocks (temb_channels=512) but unused at inference
+            s += [(pre + "temb_proj.weight", (C, 512), w, 0.0), (pre + "temb_proj.bias", (C,), b, 0.0)]
+        s += [
+            (pre + "norm2.weight", (C,), 0.1, 1.0), (pre + "norm2.bias", (C,), 0.05, 0.0),
+            (pre + "conv2.weight", (C, C, 3), w, 0.0), (pre + "conv2.bias", (C,), b, 0.0),
+        ]
+        return s
+
+    for i in range(2):
+        specs += resblock(f"decoder.backbone.prior_net.{i}.", D)
+    for i in range(cfg.depth):
+        p = f"decoder.backbone.transformers.{i}."
+        specs += [
+            (p + "att_norm.weight", (D,), 0.1, 1.0),
+            (p + "ffn_norm.weight", (D,), 0.1, 1.0),
+            (p + "att.c_attn.weight", (3 * D, D), w, 0.0),
+            (p + "att.c_proj.weight", (D, D), w, 0.0),
+            (p + "mlp.fc1.weight", (4 * D, D), w, 0.0),
+            (p + "mlp.fc2.weight", (D, 4 * D), w, 0.0),
+        ]
+    for i in range(2):
+        specs += resblock(f"decoder.backbone.post_net.{i}.", D)
+    specs += [
+        ("decoder.backbone.final_layer_norm.weight", (D,), 0.1, 1.0),
+        ("decoder.backbone.final_layer_norm.bias", (D,), 0.05, 0.0),
+    ]
+    C = D
+    for i, (u, k) in enumerate(zip(cfg.upsample_factors, cfg.kernel_sizes)):
+        p = f"upsampler.upsample_layers.{i}."
+        specs += [
+            (p + "weight_g", (C, 1, 1), 0.2, 1.0),
+            (p + "weight_v", (C, C // 2, k), w, 0.0),
+            (p + "bias", (C // 2,), b, 0.0),
+        ]
+        specs += resblock(f"upsampler.resnet_blocks.{i}.", C // 2, temb=True)
+        C //= 2
+    if cfg.upsample_factors:
+        specs += [("upsampler.out_proj.weight", (D, C), w, 0.0), ("upsampler.out_proj.bias", (D,), b, 0.0)]
+    nfft = 4 * cfg.hop_length
+    specs += [
+        ("decoder.head.out.weight", (nfft + 2, D), w, 0.0),
+        ("decoder.head.out.bias", (nfft + 2,), b, 0.0),
+    ]
+    return specs
+
+
+def codec_weights_cpu(cfg: configs.CodecArch, seed: int) -> dict[str, torch.Tensor]:
+    out = {}
+    for name, shape, scale, off in codec_tensor_specs(cfg):
+        n = int(np.prod(shape))
+        t = torch.from_numpy(synth_values(tensor_seed(seed, name), n, scale)).reshape(shape)
+        out[name] = t + off if off else t
+    # non-learned buffers that the reference state dict also carries
+    nfft = 4 * cfg.hop_length
+    out["decoder.head.istft.window"] = torch.hann_window(nfft)
+    D = cfg.vq_dim
+    out["decoder.quantizer.project_in.weight"] = torch.zeros(8, D)
+    out["decoder.quantizer.project_in.bias"] = torch.zeros(8)
+    return out
+
+
+# ------------------------------------------------------------------------ inputs -------
+
+def synthetic_prompt(vocab: configs.SpeechVocab, utt: int, n_text_tokens: int, n_prompt_codes: int,
+                     rng_base: int = 1234) -> list[int]:
+    """Prompt ids shaped like InferencePromptCompiler output (tts/core/prompting.py:124-154):
+    BOS + instruction + <|text_prompt_start|> text <|text_prompt_end|> '\\n' <|speech_start|>
+    + prompt speech codes."""
+    rng = np.random.default_rng(rng_base + utt)
+    text_hi = vocab.text_vocab
+    ids = [vocab.bos_id]
+    ids += rng.integers(0, text_hi, size=8).tolist()  # "Convert the text to speech:"
+    ids += [vocab.text_prompt_start_id]
+    ids += rng.integers(0, text_hi, size=n_text_tokens).tolist()
+    ids += [vocab.text_prompt_end_id, vocab.newline_id, vocab.speech_start_id]
+    codes = rng.integers(0, vocab.codebook_size, size=n_prompt_codes)
+    ids += [vocab.code_to_id(int(c)) for c in codes]
+    return [int(x) for x in ids]
