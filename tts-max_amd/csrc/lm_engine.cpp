@@ -234,7 +234,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.q_rot.alloc((size_t)R * H * D * 2);
   w.act.alloc((size_t)R * FF * 2);
   w.last_x.alloc((size_t)B * HID * 2);
-  w.split_decode = (B <= 4) ? 64 : 256;
+  w.split_decode = decode_split(D);
   w.nsplit_decode = (S + w.split_decode - 1) / w.split_decode;
   w.split_prefill = 512;  // = the kv block of torch's CPU flash kernel (kv_split_size)
   w.nsplit_prefill = (S + w.split_prefill - 1) / w.split_prefill;
@@ -274,7 +274,7 @@ struct Ctx {
     for (int r0 = 0; r0 < rows; r0 += kPrefillChunk) {
       const int m = std::min(kPrefillChunk, rows - r0);
       WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
-      const bf16_t* xin = x + (size_t)r0 * K;
+      const bf16_t* xin = x ? x + (size_t)r0 * K : nullptr;
       bool norm = normw != nullptr;
       if (norm && !p.a_lds) {  // fused RMSNorm needs the rows in LDS: normalise separately
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
@@ -320,15 +320,25 @@ struct Ctx {
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(),
            nullptr, EPI_STORE);
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
+      // decode with few rows: the o_proj prologue merges the attention chunks itself
+      const bool fuse_combine = decode && rows <= kPrefillChunk &&
+                                plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
       if (decode) {
-        launch_attn_decode(a, true, s);
+        launch_attn_decode_step(a, s);
       } else {
         launch_rope_append(a, s);
         launch_attn_decode(a, false, s);
       }
-      launch_attn_combine(a, s);
-      gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
-           w.x.as<bf16_t>(), EPI_RESID);
+      if (fuse_combine) {
+        WgemmArgs ex;
+        ex.attn_o = a.part_o; ex.attn_ml = a.part_ml; ex.attn_pos = pos;
+        ex.attn_split = a.split; ex.attn_nsplit = a.nsplit; ex.attn_D = a.D;
+        gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &ex);
+      } else {
+        launch_attn_combine(a, s);
+        gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
+             w.x.as<bf16_t>(), EPI_RESID);
+      }
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),

@@ -52,9 +52,12 @@ void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, hipStream_t s, int 
 }
 
 // ---------------------------------------------------------------- the GEMM kernel -----
-constexpr int WG_THREADS = 256;
-constexpr int KU = 8;  // k-tiles per pipeline stage (8 KiB of weights per wave per stage)
-
+// One workgroup = WAVES waves; KSPLIT consecutive waves split the K range of one unit
+// (a unit = NG n-tiles of 16 output columns), WAVES/KSPLIT units run side by side, and
+// the workgroup walks units grid-stride.  Each wave streams its weight tiles in stages
+// of KU tiles (KU KiB), double-buffered, and the stream never stops: the first stage is
+// issued before the A-operand prologue (RMSNorm / attention combine), and the last stage
+// of a unit prefetches the first stage of the wave's next unit.
 TTS_DEV bf16x8_t as_bf16x8(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 // Better (value, index): larger value wins, lower index on ties (torch.argmax semantics).
@@ -62,34 +65,54 @@ TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
 
-template <int MT, int NG, int KSPLIT, bool A_LDS, bool NORM, int EPI>
-__global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
+constexpr int A_GLOBAL = 0, A_LDS = 1, A_ATTN = 2;
+
+// MT_MAX: compile-time bound on 16-row m-tiles (1 for decode, 4 for up to 64 rows)
+template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI>
+__global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int UPW = 4 / KSPLIT;  // units processed concurrently by one workgroup
+  constexpr int NT = WAVES * 64;
+  constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int kpart = wave % KSPLIT;
   const int ugrp = wave / KSPLIT;
   const int M = a.M;
+  const int mtn = (M + 15) >> 4;
   const int KT = a.K >> 5;
   const int units = (a.N >> 4) / NG;
   const int kt_per = KT / KSPLIT;
   const int kt0 = kpart * kt_per;
+  const int kend = kt0 + kt_per;
   const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
+  const int ustride = gridDim.x * UPW;
 
   bf16_t* xs = (bf16_t*)smem;
-  const size_t xs_bytes = A_LDS ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
-  float* red = (float*)(smem + xs_bytes);  // [4 waves][NG*MT*4][64] split-K partials
-  float* scal = red + 4 * NG * MT * 4 * 64;  // small scratch (block reductions)
+  const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
+  float* red = (float*)(smem + xs_bytes);  // [WAVES][NG*MT_MAX*4][64] split-K partials
+  float* scal = red + WAVES * NG * MT_MAX * 4 * 64;
 
-  // ---- prologue: stage the A rows (optionally RMSNorm'ed) in LDS once per workgroup
-  if constexpr (A_LDS) {
+  // ---- start the weight stream before anything else
+  int u = blockIdx.x * UPW + ugrp;
+  u32x4_t wb[KU][NG];
+  auto wptr = [&](int uu, int g) {
+    return (const u32x4_t*)(a.w + ((size_t)(uu * NG + g) * KT) * 512) + lane;
+  };
+  if (u < units) {
+#pragma unroll
+    for (int kk = 0; kk < KU; ++kk)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) wb[kk][g] = __builtin_nontemporal_load(wptr(u, g) + (kt0 + kk) * 64);
+  }
+
+  // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
+  if constexpr (ASRC == A_LDS) {
     for (int m = 0; m < M; ++m) {
       const bf16_t* xr = a.x + (size_t)m * a.ldx;
       float r = 1.0f;
       if constexpr (NORM) {
         float ss = 0.f;
-        for (int k = threadIdx.x * 8; k < a.K; k += WG_THREADS * 8) {
+        for (int k = threadIdx.x * 8; k < a.K; k += NT * 8) {
           const u32x4_t v = *(const u32x4_t*)(xr + k);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -100,7 +123,7 @@ __global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
         ss = block_sum(ss, scal);
         r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
       }
-      for (int k = threadIdx.x * 8; k < a.K; k += WG_THREADS * 8) {
+      for (int k = threadIdx.x * 8; k < a.K; k += NT * 8) {
         u32x4_t v = *(const u32x4_t*)(xr + k);
         if constexpr (NORM) {
           const u32x4_t g = *(const u32x4_t*)(a.normw + k);
@@ -115,94 +138,115 @@ __global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
       }
     }
     __syncthreads();
+  } else if constexpr (ASRC == A_ATTN) {
+    // o[m][h*D+d] = sum_s o_s e^(m_s - M) / sum_s l_s e^(m_s - M) over this row's chunks
+    const int D = a.attn_D;
+    for (int e = threadIdx.x; e < M * a.K; e += NT) {
+      const int m = e / a.K, hd = e % a.K, h = hd / D, d = hd % D;
+      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
+      const size_t pb = ((size_t)m * (a.K / D) + h) * a.attn_nsplit;
+      float mx = -INFINITY;
+      for (int s = 0; s < ns; ++s) mx = fmaxf(mx, a.attn_ml[(pb + s) * 2]);
+      float l = 0.f, o = 0.f;
+      for (int s = 0; s < ns; ++s) {
+        const float f = expf(a.attn_ml[(pb + s) * 2] - mx);
+        l += a.attn_ml[(pb + s) * 2 + 1] * f;
+        o += a.attn_o[(pb + s) * D + d] * f;
+      }
+      xs[(size_t)m * ldxs + hd] = f2bf(o / l);
+    }
+    __syncthreads();
   }
 
   const int arow = lane & 15;
   const int akoff = 8 * (lane >> 4);
 
   // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
-  float best_v[MT][4];
-  int best_i[MT][4];
+  float best_v[MT_MAX][4];
+  int best_i[MT_MAX][4];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+  for (int mt = 0; mt < MT_MAX; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { best_v[mt][r] = -INFINITY; best_i[mt][r] = 0x7fffffff; }
 
-  for (int ubase = blockIdx.x * UPW; ubase < units; ubase += gridDim.x * UPW) {
-    const int u = ubase + ugrp;
+  for (int ubase = blockIdx.x * UPW; ubase < units; ubase += ustride) {
+    u = ubase + ugrp;
     const bool active = u < units;
-    f32x4_t acc[NG][MT];
+    f32x4_t acc[NG][MT_MAX];
 #pragma unroll
     for (int g = 0; g < NG; ++g)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     if (active) {
-      const u32x4_t* wt[NG];
-#pragma unroll
-      for (int g = 0; g < NG; ++g)
-        wt[g] = (const u32x4_t*)(a.w + ((size_t)(u * NG + g) * KT) * 512) + lane;
-      const int kend = kt0 + kt_per;
-      u32x4_t wb[KU][NG];
-#pragma unroll
-      for (int kk = 0; kk < KU; ++kk)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) wb[kk][g] = __builtin_nontemporal_load(wt[g] + (kt0 + kk) * 64);
-
+      const int unext = u + ustride;
       for (int kt = kt0; kt < kend; kt += KU) {
-        // prefetch the next stage (clamped: the last stage re-reads itself, never out of range)
-        const int ktn = (kt + KU < kend) ? kt + KU : kt;
+        // next stage: same unit, else the first stage of the wave's next unit
+        int nu = u, nk = kt + KU;
+        if (nk >= kend) { nu = unext; nk = kt0; }
+        const bool has_next = nu < units;
         u32x4_t wn[KU][NG];
+        if (has_next) {
 #pragma unroll
-        for (int kk = 0; kk < KU; ++kk)
+          for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
-          for (int g = 0; g < NG; ++g) wn[kk][g] = __builtin_nontemporal_load(wt[g] + (ktn + kk) * 64);
+            for (int g = 0; g < NG; ++g) wn[kk][g] = __builtin_nontemporal_load(wptr(nu, g) + (nk + kk) * 64);
+        }
 
 #pragma unroll
         for (int kk = 0; kk < KU; ++kk) {
           const int k = (kt + kk) * 32 + akoff;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int m = mt * 16 + arow;
-            u32x4_t av = u32x4_t{0u, 0u, 0u, 0u};
-            if (m < M) {
-              if constexpr (A_LDS) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
-              else av = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
-            }
-            const bf16x8_t af = as_bf16x8(av);
+          for (int mt = 0; mt < MT_MAX; ++mt) {
+            if (mt < mtn) {
+              const int m = mt * 16 + arow;
+              u32x4_t av = u32x4_t{0u, 0u, 0u, 0u};
+              if (m < M) {
+                if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
+                else av = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+              }
+              const bf16x8_t af = as_bf16x8(av);
 #pragma unroll
-            for (int g = 0; g < NG; ++g)
-              acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, as_bf16x8(wb[kk][g]),
-                                                                   acc[g][mt], 0, 0, 0);
+              for (int g = 0; g < NG; ++g)
+                acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, as_bf16x8(wb[kk][g]),
+                                                                     acc[g][mt], 0, 0, 0);
+            }
           }
         }
+        if (has_next) {
 #pragma unroll
-        for (int kk = 0; kk < KU; ++kk)
+          for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
-          for (int g = 0; g < NG; ++g) wb[kk][g] = wn[kk][g];
+            for (int g = 0; g < NG; ++g) wb[kk][g] = wn[kk][g];
+        }
       }
     }
 
     // ---- split-K combine through LDS, fixed order (deterministic)
     if constexpr (KSPLIT > 1) {
-      float* myred = red + (size_t)wave * (NG * MT * 4 * 64);
+      constexpr int PS = NG * MT_MAX * 4 * 64;
+      float* myred = red + (size_t)wave * PS;
 #pragma unroll
       for (int g = 0; g < NG; ++g)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < MT_MAX; ++mt)
+          if (mt < mtn) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) myred[((g * MT + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
+            for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
+          }
       __syncthreads();
       if (kpart == 0) {
 #pragma unroll
         for (int p = 1; p < KSPLIT; ++p) {
-          const float* o = red + (size_t)(wave + p) * (NG * MT * 4 * 64);
+          const float* o = red + (size_t)(wave + p) * PS;
 #pragma unroll
           for (int g = 0; g < NG; ++g)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+            for (int mt = 0; mt < MT_MAX; ++mt)
+              if (mt < mtn) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) acc[g][mt][r] += o[((g * MT + mt) * 4 + r) * 64 + lane];
+                for (int r = 0; r < 4; ++r) acc[g][mt][r] += o[((g * MT_MAX + mt) * 4 + r) * 64 + lane];
+              }
         }
       }
       __syncthreads();
@@ -210,27 +254,25 @@ __global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
 
     // ---- epilogue (lane owns column n, rows m = mt*16 + 4*(lane>>4) + r)
     if (kpart == 0 && active) {
+      const int n = u * 16 + (lane & 15);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int mt = 0; mt < MT_MAX; ++mt) {
+        if (mt >= mtn) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = mt * 16 + 4 * (lane >> 4) + r;
           if (m >= M) continue;
           if constexpr (EPI == EPI_STORE) {
-            const int n = u * 16 + (lane & 15);
             a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
           } else if constexpr (EPI == EPI_RESID) {
-            const int n = u * 16 + (lane & 15);
             bf16_t* p = a.resid + (size_t)m * a.ldo + n;
             *p = f2bf(bf2f(*p) + rbf(acc[0][mt][r]));
           } else if constexpr (EPI == EPI_SWIGLU) {
             // unit u = (gate tile, up tile) pair for intermediate columns u*16 .. u*16+15
-            const int n = u * 16 + (lane & 15);
             const float gt = rbf(acc[0][mt][r]);
-            const float up = rbf(acc[1][mt][r]);
+            const float up = rbf(acc[NG - 1][mt][r]);
             a.out[(size_t)m * a.ldo + n] = f2bf(rbf(silu_f(gt)) * up);
           } else if constexpr (EPI == EPI_LOGITS) {
-            const int n = u * 16 + (lane & 15);
             float v = rbf(acc[0][mt][r]);  // logits are materialised in bf16, then .float()
             const uint32_t bits = a.seen[(size_t)m * a.seen_stride + (n >> 5)];
             if ((bits >> (n & 31)) & 1u) v = (v < 0.f) ? v * a.penalty : v / a.penalty;
@@ -245,7 +287,7 @@ __global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
   if constexpr (EPI == EPI_LOGITS) {
     // lanes sharing (lane >> 4) hold the same rows: butterfly over the 16 columns
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT_MAX; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -256,23 +298,23 @@ __global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
         }
     // across the unit-groups of the workgroup (only kpart==0 waves hold results)
     float* rv = red;
-    int* ri = (int*)(red + 4 * MT * 16);
+    int* ri = (int*)(red + UPW * MT_MAX * 16);
     __syncthreads();
     if (kpart == 0 && (lane & 15) == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT_MAX; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = mt * 16 + 4 * (lane >> 4) + r;
-          rv[ugrp * MT * 16 + m] = best_v[mt][r];
-          ri[ugrp * MT * 16 + m] = best_i[mt][r];
+          rv[ugrp * MT_MAX * 16 + m] = best_v[mt][r];
+          ri[ugrp * MT_MAX * 16 + m] = best_i[mt][r];
         }
     }
     __syncthreads();
-    for (int m = threadIdx.x; m < M; m += WG_THREADS) {
+    for (int m = threadIdx.x; m < M; m += NT) {
       float v = rv[m];
       int i = ri[m];
-      for (int g = 1; g < UPW; ++g) argmax_merge(v, i, rv[g * MT * 16 + m], ri[g * MT * 16 + m]);
+      for (int g = 1; g < UPW; ++g) argmax_merge(v, i, rv[g * MT_MAX * 16 + m], ri[g * MT_MAX * 16 + m]);
       a.part_val[(size_t)m * a.part_stride + blockIdx.x] = v;
       a.part_idx[(size_t)m * a.part_stride + blockIdx.x] = i;
     }
@@ -280,46 +322,48 @@ __global__ __launch_bounds__(WG_THREADS) void wgemm_kernel(WgemmArgs a) {
 }
 
 // ---------------------------------------------------------------- host dispatch -------
-template <int MT, int NG, int KSPLIT, bool A_LDS, bool NORM, int EPI>
+// Launch shapes (WAVES, KU, KSPLIT): a small fixed table keeps the instantiation count low.
+enum { CFG_WIDE = 0, CFG_K2 = 1, CFG_K8 = 3, CFG_K4 = 4 };
+
+template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI>
 static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
-  size_t lds = A_LDS ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
-  lds += (size_t)(4 * NG * MT * 4 * 64 + 64) * sizeof(float);
-  hipLaunchKernelGGL((wgemm_kernel<MT, NG, KSPLIT, A_LDS, NORM, EPI>), dim3(grid),
-                     dim3(WG_THREADS), lds, s, a);
+  const int mt = a.M <= 16 ? 1 : 4;
+  size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
+  lds += (size_t)(WAVES * NG * mt * 4 * 64 + 64) * sizeof(float);
+  if (mt == 1)
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
+                       dim3(WAVES * 64), lds, s, a);
+  else
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 4, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
+                       dim3(WAVES * 64), lds, s, a);
 }
 
-template <int MT, int NG, bool A_LDS, bool NORM, int EPI>
-static void launch_ks(const WgemmArgs& a, int ksplit, int grid, hipStream_t s) {
-  if (ksplit == 4) launch_one<MT, NG, 4, A_LDS, NORM, EPI>(a, grid, s);
-  else if (ksplit == 2) launch_one<MT, NG, 2, A_LDS, NORM, EPI>(a, grid, s);
-  else launch_one<MT, NG, 1, A_LDS, NORM, EPI>(a, grid, s);
-}
-
-template <int NG, bool A_LDS, bool NORM, int EPI>
-static void launch_mt(const WgemmArgs& a, int mt, int ksplit, int grid, hipStream_t s) {
-  switch (mt) {
-    case 1: launch_ks<1, NG, A_LDS, NORM, EPI>(a, ksplit, grid, s); break;
-    case 2: launch_ks<2, NG, A_LDS, NORM, EPI>(a, ksplit, grid, s); break;
-    case 3: launch_ks<3, NG, A_LDS, NORM, EPI>(a, ksplit, grid, s); break;
-    default: launch_ks<4, NG, A_LDS, NORM, EPI>(a, ksplit, grid, s); break;
+template <int NG, int ASRC, bool NORM, int EPI>
+static void launch_cfg(const WgemmArgs& a, int cfg, int grid, hipStream_t s) {
+  switch (cfg) {
+    case CFG_WIDE: launch_one<4, 8, NG, 1, ASRC, NORM, EPI>(a, grid, s); break;
+    case CFG_K2: launch_one<4, 8, NG, 2, ASRC, NORM, EPI>(a, grid, s); break;
+    case CFG_K8: launch_one<8, 8, NG, 8, ASRC, NORM, EPI>(a, grid, s); break;
+    default: launch_one<4, 8, NG, 4, ASRC, NORM, EPI>(a, grid, s); break;
   }
 }
 
-// Picks split-K and grid so that small-N projections still cover the 256 CUs and
-// large-N ones (lm_head, MLP) stream whole n-tiles per wave.
+// Chooses the launch shape so that every CU has work and enough bytes in flight: large-N
+// GEMMs (lm_head, MLP) stream whole n-tiles per wave; small-N projections split K across
+// the waves of a workgroup (and use 8-wave workgroups when only ~128 units exist).
 WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   WgemmPlan p;
   const int NG = (epi == EPI_SWIGLU) ? 2 : 1;
   const int units = (N / 16) / NG;
   const int KT = K / 32;
   p.a_lds = ((size_t)M * (K + 8) * 2) <= 80 * 1024;
-  int ks = 1;
-  // enough units for every wave of every CU to own whole tiles? else split K in-workgroup
-  if (units < num_cu * 4) ks = 2;
-  if (units < num_cu * 2) ks = 4;
-  while (ks > 1 && (KT % (ks * KU)) != 0) ks >>= 1;
-  p.ksplit = ks;
-  const int upw = 4 / ks;
+  int cfg, upw;
+  if (units >= num_cu * 4) { cfg = CFG_WIDE; upw = 4; }
+  else if (units >= num_cu * 2 && KT % 16 == 0) { cfg = CFG_K2; upw = 2; }
+  else if (KT % 64 == 0) { cfg = CFG_K8; upw = 1; }
+  else if (KT % 32 == 0) { cfg = CFG_K4; upw = 1; }
+  else { cfg = CFG_WIDE; upw = 4; }
+  p.cfg = cfg;
   int grid = (units + upw - 1) / upw;
   const int cap = (epi == EPI_LOGITS) ? LOGITS_MAX_PARTS : num_cu * 8;
   if (grid > cap) grid = cap;
@@ -329,28 +373,33 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
 
 bool wgemm_supported(int M, int N, int K, int epi) {
   const int NG = (epi == EPI_SWIGLU) ? 2 : 1;
-  return M >= 1 && M <= 64 && (N % (16 * NG)) == 0 && (K % (32 * KU)) == 0;
+  return M >= 1 && M <= 64 && (N % (16 * NG)) == 0 && (K % 256) == 0;
 }
 
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s) {
-  const int mt = (a.M + 15) / 16;
-  const bool lds = p.a_lds;
-#define TTS_DISPATCH(NGV, EPIV)                                                        \
-  do {                                                                                 \
-    if (lds) {                                                                         \
-      if (norm) launch_mt<NGV, true, true, EPIV>(a, mt, p.ksplit, p.grid, s);          \
-      else launch_mt<NGV, true, false, EPIV>(a, mt, p.ksplit, p.grid, s);              \
-    } else {                                                                           \
-      launch_mt<NGV, false, false, EPIV>(a, mt, p.ksplit, p.grid, s);                  \
-    }                                                                                  \
-  } while (0)
+  const int c = p.cfg;
+  const bool attn = a.attn_o != nullptr;
   switch (epi) {
-    case EPI_STORE: TTS_DISPATCH(1, EPI_STORE); break;
-    case EPI_RESID: TTS_DISPATCH(1, EPI_RESID); break;
-    case EPI_SWIGLU: TTS_DISPATCH(2, EPI_SWIGLU); break;
-    case EPI_LOGITS: TTS_DISPATCH(1, EPI_LOGITS); break;
+    case EPI_STORE:
+      if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_STORE>(a, c, p.grid, s);
+      else if (norm) launch_cfg<1, A_LDS, true, EPI_STORE>(a, c, p.grid, s);
+      else launch_cfg<1, A_LDS, false, EPI_STORE>(a, c, p.grid, s);
+      break;
+    case EPI_RESID:
+      if (attn) launch_cfg<1, A_ATTN, false, EPI_RESID>(a, c, p.grid, s);
+      else if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_RESID>(a, c, p.grid, s);
+      else launch_cfg<1, A_LDS, false, EPI_RESID>(a, c, p.grid, s);
+      break;
+    case EPI_SWIGLU:
+      if (!p.a_lds) launch_cfg<2, A_GLOBAL, false, EPI_SWIGLU>(a, c, p.grid, s);
+      else if (norm) launch_cfg<2, A_LDS, true, EPI_SWIGLU>(a, c, p.grid, s);
+      else launch_cfg<2, A_LDS, false, EPI_SWIGLU>(a, c, p.grid, s);
+      break;
+    case EPI_LOGITS:  // the lm_head always carries the final RMSNorm (fused, or applied before)
+      if (!p.a_lds || !norm) launch_cfg<1, A_GLOBAL, false, EPI_LOGITS>(a, c, p.grid, s);
+      else launch_cfg<1, A_LDS, true, EPI_LOGITS>(a, c, p.grid, s);
+      break;
   }
-#undef TTS_DISPATCH
 }
 
 }  // namespace tts

@@ -29,10 +29,16 @@ struct WgemmArgs {
   float* part_val = nullptr;      // [M][part_stride]
   int* part_idx = nullptr;
   int part_stride = 0;
+  // A operand = attention output combined from split-K chunk partials (o_proj prologue);
+  // K = num_heads * attn_D, chunk layout as AttnArgs::part_o / part_ml
+  const float* attn_o = nullptr;
+  const float* attn_ml = nullptr;
+  const int* attn_pos = nullptr;
+  int attn_split = 0, attn_nsplit = 0, attn_D = 0;
 };
 
 struct WgemmPlan {
-  int ksplit = 1;
+  int cfg = 0;   // launch shape (waves, stage depth, in-workgroup split-K): lm_gemm.hip
   int grid = 1;
   bool a_lds = true;
 };
@@ -78,6 +84,9 @@ struct AttnArgs {
 };
 void launch_rope_append(const AttnArgs& a, hipStream_t s);       // prefill: rope q,k; append k,v
 void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
+// decode step: register-streamed chunks of decode_split(D) positions, KV append fused
+int decode_split(int D);
+void launch_attn_decode_step(const AttnArgs& a, hipStream_t s);
 void launch_attn_combine(const AttnArgs& a, hipStream_t s);
 
 // ---- sampling / bookkeeping (lm_ops.hip)
