@@ -16,81 +16,97 @@
 namespace tts {
 
 // ------------------------------------------------------------------ fp32 MFMA GEMM ----
-constexpr int GBM = 128, GBN = 128, GBK = 16;
-constexpr int GLS = 130;  // LDS row stride (floats): conflict-free transposed stores
+// Tile TM x TN x 16, four waves in a 2x2 grid, each wave (TM/2) x (TN/2) built from
+// 32x32 v_mfma_f32_32x32x2_f32 tiles.  Operands are staged k-major in LDS (row stride
+// TM+2 floats: the transposed stores of one wave-instruction hit 32 distinct banks) so an
+// MFMA operand read is 32 consecutive floats.  The next K tile is loaded into registers
+// while the current one is consumed.  64x64 tiles are used when 128x128 would leave CUs
+// idle (the codec's T ~ 500-2000 rows).
+constexpr int GBK = 16;
 
+template <int TM, int TN>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
-  __shared__ float As[GBK * GLS];
-  __shared__ float Bs[GBK * GLS];
+  constexpr int LSA = TM + 2, LSB = TN + 2;
+  constexpr int AV = TM * GBK / 256 / 4;  // float4 per thread for the A tile (1 or 2)
+  constexpr int BV = TN * GBK / 256 / 4;
+  constexpr int MI = TM / 64, NJ = TN / 64;  // 32x32 MFMA tiles per wave
+  __shared__ float As[GBK * LSA];
+  __shared__ float Bs[GBK * LSB];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware tile order: consecutive tiles of one A row-block go to one XCD (speed only)
-  const int nbn = (g.N + GBN - 1) / GBN;
-  const int bid = blockIdx.x;
-  const int m0 = (bid / nbn) * GBM, n0 = (bid % nbn) * GBN;
-  // global->LDS staging map: thread loads 8 consecutive k of one row (2 x float4)
-  const int lrow = t >> 1, lk = (t & 1) * 8;
-  const int ar = m0 + lrow, br = n0 + lrow;
-  const float* ap = g.A + (size_t)ar * g.lda + lk;
-  const float* bp = g.B + (size_t)br * g.K + lk;
+  const int nbn = (g.N + TN - 1) / TN;
+  const int m0 = (blockIdx.x / nbn) * TM, n0 = (blockIdx.x % nbn) * TN;
+  // staging map: thread -> (row, 4*AV consecutive k)
+  const int arow = t / (GBK / (4 * AV)), ak = (t % (GBK / (4 * AV))) * 4 * AV;
+  const int brow = t / (GBK / (4 * BV)), bk = (t % (GBK / (4 * BV))) * 4 * BV;
+  const int ar = m0 + arow, br = n0 + brow;
+  const float* ap = g.A + (size_t)ar * g.lda + ak;
+  const float* bp = g.B + (size_t)br * g.K + bk;
   const bool aok = ar < g.M, bok = br < g.N;
-  f32x16_t acc[2][2];
+  f32x16_t acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float4 ra0, ra1, rb0, rb1;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  ra0 = aok ? *(const float4*)(ap) : z4;
-  ra1 = aok ? *(const float4*)(ap + 4) : z4;
-  rb0 = bok ? *(const float4*)(bp) : z4;
-  rb1 = bok ? *(const float4*)(bp + 4) : z4;
+  float4 ra[AV], rb[BV];
+#pragma unroll
+  for (int v = 0; v < AV; ++v) ra[v] = aok ? *(const float4*)(ap + 4 * v) : z4;
+#pragma unroll
+  for (int v = 0; v < BV; ++v) rb[v] = bok ? *(const float4*)(bp + 4 * v) : z4;
   for (int k0 = 0; k0 < g.K; k0 += GBK) {
     __syncthreads();
-    const float av[8] = {ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w};
-    const float bv[8] = {rb0.x, rb0.y, rb0.z, rb0.w, rb1.x, rb1.y, rb1.z, rb1.w};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      As[(lk + j) * GLS + lrow] = av[j];
-      Bs[(lk + j) * GLS + lrow] = bv[j];
+    for (int v = 0; v < AV; ++v) {
+      As[(ak + 4 * v + 0) * LSA + arow] = ra[v].x;
+      As[(ak + 4 * v + 1) * LSA + arow] = ra[v].y;
+      As[(ak + 4 * v + 2) * LSA + arow] = ra[v].z;
+      As[(ak + 4 * v + 3) * LSA + arow] = ra[v].w;
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      Bs[(bk + 4 * v + 0) * LSB + brow] = rb[v].x;
+      Bs[(bk + 4 * v + 1) * LSB + brow] = rb[v].y;
+      Bs[(bk + 4 * v + 2) * LSB + brow] = rb[v].z;
+      Bs[(bk + 4 * v + 3) * LSB + brow] = rb[v].w;
     }
     __syncthreads();
     if (k0 + GBK < g.K) {  // prefetch next K tile while the MFMAs run
       const int kn = k0 + GBK;
-      ra0 = aok ? *(const float4*)(ap + kn) : z4;
-      ra1 = aok ? *(const float4*)(ap + kn + 4) : z4;
-      rb0 = bok ? *(const float4*)(bp + kn) : z4;
-      rb1 = bok ? *(const float4*)(bp + kn + 4) : z4;
+#pragma unroll
+      for (int v = 0; v < AV; ++v) ra[v] = aok ? *(const float4*)(ap + kn + 4 * v) : z4;
+#pragma unroll
+      for (int v = 0; v < BV; ++v) rb[v] = bok ? *(const float4*)(bp + kn + 4 * v) : z4;
     }
 #pragma unroll
     for (int kk = 0; kk < GBK / 2; ++kk) {
       const int kr = 2 * kk + (lane >> 5);
-      float a[2], b[2];
+      float a[MI], b[NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[kr * GLS + wm * 64 + i * 32 + (lane & 31)];
+      for (int i = 0; i < MI; ++i) a[i] = As[kr * LSA + wm * (TM / 2) + i * 32 + (lane & 31)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[kr * GLS + wn * 64 + j * 32 + (lane & 31)];
+      for (int j = 0; j < NJ; ++j) b[j] = Bs[kr * LSB + wn * (TN / 2) + j * 32 + (lane & 31)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
   // epilogue: lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * (TN / 2) + j * 32 + (lane & 31);
     if (n >= g.N) continue;
     const float bias = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int m = m0 + wm * (TM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= g.M) continue;
         float v = acc[i][j][r] + bias;
         if (g.act == 1) v = v / (1.0f + expf(-v));
@@ -101,8 +117,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
 }
 
 void launch_gemm_f32(const GemmF32Args& g, hipStream_t s) {
-  const int grid = ((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN);
-  hipLaunchKernelGGL(gemm_f32_kernel, dim3(grid), dim3(256), 0, s, g);
+  const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+  if (big >= 256) {
+    hipLaunchKernelGGL((gemm_f32_kernel<128, 128>), dim3(big), dim3(256), 0, s, g);
+  } else {
+    const int grid = ((g.M + 63) / 64) * ((g.N + 63) / 64);
+    hipLaunchKernelGGL((gemm_f32_kernel<64, 64>), dim3(grid), dim3(256), 0, s, g);
+  }
 }
 
 // ------------------------------------------------------------------ small kernels -----

@@ -560,6 +560,12 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = 1.1f; ex.eos_mask = st.eos_mask;
   ex.part_val = e->w.lpart_v.as<float>(); ex.part_idx = e->w.lpart_i.as<int>();
   ex.part_stride = LOGITS_MAX_PARTS;
+  // attention chunk partials for the fused o_proj prologue
+  launch_attn_decode_step(aa, s);
+  const bool fuse_o = plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
+  WgemmArgs exo;
+  exo.attn_o = aa.part_o; exo.attn_ml = aa.part_ml; exo.attn_pos = e->w.row_pos.as<int>();
+  exo.attn_split = aa.split; exo.attn_nsplit = aa.nsplit; exo.attn_D = aa.D;
   double b = 0;
   const double act_rw = 2.0 * rows;
   auto launch = [&]() {
@@ -568,9 +574,15 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr, EPI_STORE);
         b = 2.0 * QKV * HID + act_rw * (HID + QKV) + 2.0 * HID;
         break;
-      case 1:
-        X.gemm(e->w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID);
-        b = 2.0 * HID * HD + act_rw * (HD + 2 * HID);
+      case 1:  // as in the decode step: attention chunks merged in the prologue when they fit
+        if (fuse_o) {
+          X.gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID, &exo);
+          b = 2.0 * HID * HD + act_rw * 2 * HID +
+              (double)rows * c.num_heads * ((ctx + aa.split - 1) / aa.split) * (c.head_dim + 2) * 4;
+        } else {
+          X.gemm(e->w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID);
+          b = 2.0 * HID * HD + act_rw * (HD + 2 * HID);
+        }
         break;
       case 2:
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, e->w.act.as<bf16_t>(), FF, nullptr, EPI_SWIGLU);
@@ -585,7 +597,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         b = 2.0 * V * HID + act_rw * HID + 2.0 * HID + rows * (V / 8.0);
         break;
       case 5:
-        launch_attn_decode(aa, true, s);
+        launch_attn_decode_step(aa, s);
         b = (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2 + act_rw * QKV;
         break;
     }

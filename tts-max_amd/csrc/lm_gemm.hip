@@ -139,21 +139,36 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
     __syncthreads();
   } else if constexpr (ASRC == A_ATTN) {
-    // o[m][h*D+d] = sum_s o_s e^(m_s - M) / sum_s l_s e^(m_s - M) over this row's chunks
-    const int D = a.attn_D;
-    for (int e = threadIdx.x; e < M * a.K; e += NT) {
-      const int m = e / a.K, hd = e % a.K, h = hd / D, d = hd % D;
+    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
+    // phase 1: one thread per (row, head) turns the chunk statistics into factors (LDS);
+    // phase 2: every thread merges its (row, head, dim) elements with independent loads.
+    const int D = a.attn_D, H = a.K / D, NS = a.attn_nsplit;
+    float* fac = (float*)(smem + xs_bytes) + WAVES * NG * MT_MAX * 4 * 64 + 64;
+    for (int mh = threadIdx.x; mh < M * H; mh += NT) {
+      const int m = mh / H;
       const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
-      const size_t pb = ((size_t)m * (a.K / D) + h) * a.attn_nsplit;
+      const float* ml = a.attn_ml + (size_t)mh * NS * 2;
       float mx = -INFINITY;
-      for (int s = 0; s < ns; ++s) mx = fmaxf(mx, a.attn_ml[(pb + s) * 2]);
-      float l = 0.f, o = 0.f;
+      for (int s = 0; s < ns; ++s) mx = fmaxf(mx, ml[2 * s]);
+      float l = 0.f;
       for (int s = 0; s < ns; ++s) {
-        const float f = expf(a.attn_ml[(pb + s) * 2] - mx);
-        l += a.attn_ml[(pb + s) * 2 + 1] * f;
-        o += a.attn_o[(pb + s) * D + d] * f;
+        const float f = expf(ml[2 * s] - mx);
+        fac[mh * NS + s] = f;
+        l += ml[2 * s + 1] * f;
       }
-      xs[(size_t)m * ldxs + hd] = f2bf(o / l);
+      const float il = 1.0f / l;
+      for (int s = 0; s < ns; ++s) fac[mh * NS + s] *= il;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < M * a.K; e += NT) {
+      const int m = e / a.K, hd = e % a.K, mh = m * H + hd / D, d = hd % D;
+      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
+      const float* po = a.attn_o + (size_t)mh * NS * D + d;
+      const float* f = fac + mh * NS;
+      float o = 0.f;
+#pragma unroll 4
+      for (int s = 0; s < ns; ++s) o += po[(size_t)s * D] * f[s];
+      xs[(size_t)m * ldxs + hd] = f2bf(o);
     }
     __syncthreads();
   }
@@ -323,19 +338,21 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 
 // ---------------------------------------------------------------- host dispatch -------
 // Launch shapes (WAVES, KU, KSPLIT): a small fixed table keeps the instantiation count low.
-enum { CFG_WIDE = 0, CFG_K2 = 1, CFG_K8 = 3, CFG_K4 = 4 };
+enum { CFG_WIDE = 0, CFG_K2 = 1, CFG_K8 = 3, CFG_K4 = 4, CFG_K4W8 = 5, CFG_K16 = 6 };
 
 template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI>
 static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
   const int mt = a.M <= 16 ? 1 : 4;
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
   lds += (size_t)(WAVES * NG * mt * 4 * 64 + 64) * sizeof(float);
-  if (mt == 1)
+  if (ASRC == A_ATTN) lds += (size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit * sizeof(float);
+  if (mt == 1) {
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
                        dim3(WAVES * 64), lds, s, a);
-  else
+  } else if constexpr (WAVES <= 8) {  // 16-wave shapes are planned for M <= 16 only
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 4, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
                        dim3(WAVES * 64), lds, s, a);
+  }
 }
 
 template <int NG, int ASRC, bool NORM, int EPI>
@@ -344,6 +361,8 @@ static void launch_cfg(const WgemmArgs& a, int cfg, int grid, hipStream_t s) {
     case CFG_WIDE: launch_one<4, 8, NG, 1, ASRC, NORM, EPI>(a, grid, s); break;
     case CFG_K2: launch_one<4, 8, NG, 2, ASRC, NORM, EPI>(a, grid, s); break;
     case CFG_K8: launch_one<8, 8, NG, 8, ASRC, NORM, EPI>(a, grid, s); break;
+    case CFG_K4W8: launch_one<8, 8, NG, 4, ASRC, NORM, EPI>(a, grid, s); break;
+    case CFG_K16: launch_one<16, 8, NG, 16, ASRC, NORM, EPI>(a, grid, s); break;
     default: launch_one<4, 8, NG, 4, ASRC, NORM, EPI>(a, grid, s); break;
   }
 }
@@ -359,7 +378,9 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   p.a_lds = ((size_t)M * (K + 8) * 2) <= 80 * 1024;
   int cfg, upw;
   if (units >= num_cu * 4) { cfg = CFG_WIDE; upw = 4; }
+  else if (units >= num_cu * 2 && KT % 32 == 0) { cfg = CFG_K4W8; upw = 2; }
   else if (units >= num_cu * 2 && KT % 16 == 0) { cfg = CFG_K2; upw = 2; }
+  else if (2 * units <= num_cu && KT % 128 == 0 && M <= 16) { cfg = CFG_K16; upw = 1; }
   else if (KT % 64 == 0) { cfg = CFG_K8; upw = 1; }
   else if (KT % 32 == 0) { cfg = CFG_K4; upw = 1; }
   else { cfg = CFG_WIDE; upw = 4; }
