@@ -1,6 +1,8 @@
 // capi.cpp — the extern "C" boundary (include/tts_mi355x.h, include/tts_mi355x_ops.h).
 // Every entry point catches everything: errors become a status code plus a thread-local
 // message, never an exception across the ABI.
+#include <stdlib.h>
+
 #include <string>
 
 #include "../../include/tts_mi355x.h"
@@ -63,6 +65,7 @@ tts_status tts_engine_create(int32_t device, tts_engine** out) {
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     e->num_cu = prop.multiProcessorCount;
     HIP_CHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (const char* v = getenv("TTS_PREFETCH")) e->prefetch = atoi(v) != 0;
     for (auto& v : e->ev) HIP_CHECK(hipEventCreate(&v));
     *out = reinterpret_cast<tts_engine*>(e);
   });

@@ -111,6 +111,7 @@ struct Engine {
   Codec* codec = nullptr;
   float t_prefill_ms = 0.f, t_decode_ms = 0.f;
   int decode_steps = 0;
+  bool prefetch = true;  // decode-step cache warming (env TTS_PREFETCH=0 disables; A/B only)
   ~Engine();
 };
 

@@ -313,36 +313,63 @@ struct Ctx {
   }
 
   // One transformer stack pass over `rows` rows held in w.x.
+  // Decode-step cache warming: the latency-bound launches of a layer
+  // (qkv, attention, o_proj, down) leave CUs idle; extra workgroups on those CUs read the
+  // weights the following launches will stream, so that HBM time overlaps the latency
+  // chains and the consumers find the lines in the Infinity Cache.  The layer's matrices
+  // are contiguous in the slab (wqkv | wo | wgu | wd | next layer), so each warm-up is
+  // one byte range.
+  static Prefetch pf_range(const void* base, size_t off, size_t bytes, int wgs) {
+    Prefetch p;
+    p.ptr = (const char*)base + off;
+    p.bytes = bytes;
+    p.wgs = wgs;
+    return p;
+  }
+
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
+    const bool warm = decode && e->prefetch;
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
+      const size_t wo_b = (size_t)HID * HD * 2, wgu_b = (size_t)2 * FF * HID * 2;
+      const size_t wd_b = (size_t)HID * FF * 2;
+      const size_t gu_a = wgu_b * 3 / 5;  // share of wgu warmed during attention
+      WgemmArgs exq;
+      if (warm) exq.pf = pf_range(ly.wo, 0, wo_b, 64);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(),
-           nullptr, EPI_STORE);
+           nullptr, EPI_STORE, &exq);
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
       // decode with few rows: the o_proj prologue merges the attention chunks itself
       const bool fuse_combine = decode && rows <= kPrefillChunk &&
                                 plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
       if (decode) {
+        if (warm) a.pf = pf_range(ly.wgu, 0, gu_a, 192);
         launch_attn_decode_step(a, s);
       } else {
         launch_rope_append(a, s);
         launch_attn_decode(a, false, s);
       }
+      WgemmArgs exo;
+      if (warm) exo.pf = pf_range(ly.wgu, gu_a, wgu_b - gu_a + wd_b / 2, 128);
       if (fuse_combine) {
-        WgemmArgs ex;
-        ex.attn_o = a.part_o; ex.attn_ml = a.part_ml; ex.attn_pos = pos;
-        ex.attn_split = a.split; ex.attn_nsplit = a.nsplit; ex.attn_D = a.D;
-        gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &ex);
+        exo.attn_o = a.part_o; exo.attn_ml = a.part_ml; exo.attn_pos = pos;
+        exo.attn_split = a.split; exo.attn_nsplit = a.nsplit; exo.attn_D = a.D;
+        gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &exo);
       } else {
         launch_attn_combine(a, s);
         gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
-             w.x.as<bf16_t>(), EPI_RESID);
+             w.x.as<bf16_t>(), EPI_RESID, &exo);
       }
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
+      WgemmArgs exd;
+      if (warm && l + 1 < c.num_layers) {  // next layer's norms + qkv projection
+        const LmLayer& nx = M.layers[l + 1];
+        exd.pf = pf_range(nx.ln1, 0, (size_t)(nx.wo - nx.ln1) * 2, 128);
+      }
       gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),
-           EPI_RESID);
+           EPI_RESID, &exd);
     }
   }
 

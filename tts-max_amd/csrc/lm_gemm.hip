@@ -73,6 +73,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
   constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
+  if ((int)blockIdx.x >= a.real_grid) {
+    prefetch_role(a.pf.ptr, a.pf.bytes, blockIdx.x - a.real_grid, gridDim.x - a.real_grid);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int kpart = wave % KSPLIT;
@@ -85,7 +89,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   const int kt0 = kpart * kt_per;
   const int kend = kt0 + kt_per;
   const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
-  const int ustride = gridDim.x * UPW;
+  const int ustride = a.real_grid * UPW;
 
   bf16_t* xs = (bf16_t*)smem;
   const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
@@ -397,28 +401,31 @@ bool wgemm_supported(int M, int N, int K, int epi) {
   return M >= 1 && M <= 64 && (N % (16 * NG)) == 0 && (K % 256) == 0;
 }
 
-void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s) {
+void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p, int epi, bool norm, hipStream_t s) {
+  WgemmArgs a = a_in;
+  a.real_grid = p.grid;
+  const int grid = p.grid + ((a.pf.bytes && a.pf.ptr) ? a.pf.wgs : 0);
   const int c = p.cfg;
   const bool attn = a.attn_o != nullptr;
   switch (epi) {
     case EPI_STORE:
-      if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_STORE>(a, c, p.grid, s);
-      else if (norm) launch_cfg<1, A_LDS, true, EPI_STORE>(a, c, p.grid, s);
-      else launch_cfg<1, A_LDS, false, EPI_STORE>(a, c, p.grid, s);
+      if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_STORE>(a, c, grid, s);
+      else if (norm) launch_cfg<1, A_LDS, true, EPI_STORE>(a, c, grid, s);
+      else launch_cfg<1, A_LDS, false, EPI_STORE>(a, c, grid, s);
       break;
     case EPI_RESID:
-      if (attn) launch_cfg<1, A_ATTN, false, EPI_RESID>(a, c, p.grid, s);
-      else if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_RESID>(a, c, p.grid, s);
-      else launch_cfg<1, A_LDS, false, EPI_RESID>(a, c, p.grid, s);
+      if (attn) launch_cfg<1, A_ATTN, false, EPI_RESID>(a, c, grid, s);
+      else if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_RESID>(a, c, grid, s);
+      else launch_cfg<1, A_LDS, false, EPI_RESID>(a, c, grid, s);
       break;
     case EPI_SWIGLU:
-      if (!p.a_lds) launch_cfg<2, A_GLOBAL, false, EPI_SWIGLU>(a, c, p.grid, s);
-      else if (norm) launch_cfg<2, A_LDS, true, EPI_SWIGLU>(a, c, p.grid, s);
-      else launch_cfg<2, A_LDS, false, EPI_SWIGLU>(a, c, p.grid, s);
+      if (!p.a_lds) launch_cfg<2, A_GLOBAL, false, EPI_SWIGLU>(a, c, grid, s);
+      else if (norm) launch_cfg<2, A_LDS, true, EPI_SWIGLU>(a, c, grid, s);
+      else launch_cfg<2, A_LDS, false, EPI_SWIGLU>(a, c, grid, s);
       break;
     case EPI_LOGITS:  // the lm_head always carries the final RMSNorm (fused, or applied before)
-      if (!p.a_lds || !norm) launch_cfg<1, A_GLOBAL, false, EPI_LOGITS>(a, c, p.grid, s);
-      else launch_cfg<1, A_LDS, true, EPI_LOGITS>(a, c, p.grid, s);
+      if (!p.a_lds || !norm) launch_cfg<1, A_GLOBAL, false, EPI_LOGITS>(a, c, grid, s);
+      else launch_cfg<1, A_LDS, true, EPI_LOGITS>(a, c, grid, s);
       break;
   }
 }

@@ -9,6 +9,14 @@ namespace tts {
 typedef uint16_t bf16_t;
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
+
+// Byte range warmed into the Infinity Cache by `wgs` extra workgroups of a launch
+// (prefetch_role in hip_common.h).
+struct Prefetch {
+  const void* ptr = nullptr;
+  size_t bytes = 0;
+  int wgs = 0;
+};
 constexpr int LOGITS_MAX_PARTS = 1024;  // lm_head workgroups = argmax partials per row
 
 struct WgemmArgs {
@@ -35,6 +43,8 @@ struct WgemmArgs {
   const float* attn_ml = nullptr;
   const int* attn_pos = nullptr;
   int attn_split = 0, attn_nsplit = 0, attn_D = 0;
+  Prefetch pf;        // cache warming by extra workgroups (set by the engine)
+  int real_grid = 0;  // workgroups doing the GEMM (filled in by launch_wgemm)
 };
 
 struct WgemmPlan {
@@ -81,6 +91,7 @@ struct AttnArgs {
   float* part_ml = nullptr; // [rows][H][nsplit][2] (running max, sum)
   bf16_t* q_rot = nullptr;  // prefill: roped q [rows][H*D]
   bf16_t* out = nullptr;    // [rows][H*D] bf16
+  Prefetch pf;              // decode step: cache warming by extra workgroups
 };
 void launch_rope_append(const AttnArgs& a, hipStream_t s);       // prefill: rope q,k; append k,v
 void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
