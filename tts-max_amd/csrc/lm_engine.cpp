@@ -595,7 +595,11 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   exo.attn_split = aa.split; exo.attn_nsplit = aa.nsplit; exo.attn_D = aa.D;
   double b = 0;
   const double act_rw = 2.0 * rows;
+  // launches rotate over the layers (as the decode step does), so a layer's weights are
+  // not still cached from the previous launch: the timing reflects HBM streaming
+  int it_layer = 0;
   auto launch = [&]() {
+    const LmLayer& ly = X.M.layers[it_layer++ % c.num_layers];
     switch (which) {
       case 0:
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr, EPI_STORE);

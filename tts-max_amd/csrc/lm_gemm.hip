@@ -388,6 +388,16 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   else if (KT % 64 == 0) { cfg = CFG_K8; upw = 1; }
   else if (KT % 32 == 0) { cfg = CFG_K4; upw = 1; }
   else { cfg = CFG_WIDE; upw = 4; }
+  // experiment hook (scripts/microbench.py): force a launch shape when it divides the shape
+  static const int forced = getenv("TTS_WGEMM_CFG") ? atoi(getenv("TTS_WGEMM_CFG")) : -1;
+  if (forced >= 0) {
+    const int ks[] = {1, 2, 0, 8, 4, 4, 16};
+    const int up[] = {4, 2, 0, 1, 1, 2, 1};
+    if (forced <= 6 && ks[forced] && KT % (ks[forced] * 8) == 0 && (forced != CFG_K16 || M <= 16)) {
+      cfg = forced;
+      upw = up[forced];
+    }
+  }
   p.cfg = cfg;
   int grid = (units + upw - 1) / upw;
   const int cap = (epi == EPI_LOGITS) ? LOGITS_MAX_PARTS : num_cu * 8;
