@@ -30,6 +30,33 @@ TTS_DEV uint32_t pack_bf2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
+// ---- DPP wave reductions (VALU speed; __shfl_xor lowers to ds_bpermute = LDS latency)
+template <int CTRL, int ROW_MASK = 0xf>
+TTS_DEV float dpp_mov(float old, float src) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL,
+                                                    ROW_MASK, 0xf, false));
+}
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror, row_bcast:15 (rows
+// 1,3), row_bcast:31 (rows 2,3): lane 63 ends with the full reduction; read it uniformly.
+TTS_DEV float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(0.f, v);
+  v += dpp_mov<0x4E>(0.f, v);
+  v += dpp_mov<0x141>(0.f, v);
+  v += dpp_mov<0x140>(0.f, v);
+  v += dpp_mov<0x142, 0xA>(0.f, v);
+  v += dpp_mov<0x143, 0xC>(0.f, v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+TTS_DEV float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x4E>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x141>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x140>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x142, 0xA>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x143, 0xC>(-INFINITY, v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 TTS_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -44,7 +71,7 @@ TTS_DEV float wave_max(float v) {
 // Block-wide sum for blockDim.x a multiple of 64 (<= 1024).  `red` is >= 16 floats of LDS.
 TTS_DEV float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  v = wave_sum(v);
+  v = wave_sum_dpp(v);
   __syncthreads();
   if (lane == 0) red[w] = v;
   __syncthreads();
@@ -54,7 +81,7 @@ TTS_DEV float block_sum(float v, float* red) {
 }
 TTS_DEV float block_max(float v, float* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  v = wave_max(v);
+  v = wave_max_dpp(v);
   __syncthreads();
   if (lane == 0) red[w] = v;
   __syncthreads();

@@ -369,9 +369,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
   }
 }
 
-int decode_split(int D) { return D == 64 ? 128 : 64; }  // = PPB * IT of the instances below
-
-void launch_attn_decode_step(const AttnArgs& a, hipStream_t s) {
+// (superseded by lm_attn_decode.hip: the lane-shuffle reductions above lower to
+//  ds_bpermute and serialise on LDS latency; kept only for reference / A-B runs)
+void launch_attn_decode_step_shfl(const AttnArgs& a, hipStream_t s) {
   dim3 grid(a.rows * a.KVH * a.nsplit + ((a.pf.bytes && a.pf.ptr) ? a.pf.wgs : 0));
   if (a.D == 64) hipLaunchKernelGGL((attn_decode_kernel<64, 4>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((attn_decode_kernel<128, 4>), grid, dim3(256), 0, s, a);

@@ -1,0 +1,169 @@
+// lm_attn_decode.hip — decode-step attention (one new query row per sequence, GQA 4:1),
+// with RoPE of the new q/k and the KV-cache append fused in.
+//
+// Reference: LlamaAttention.forward (transformers modeling_llama.py:217-281) at decode time:
+// apply_rotary_pos_emb in bf16 (:138-160), DynamicCache.update (append), SDPA with
+// scale D^-0.5 and flash numerics (p = exp(s - max) in fp32, P rounded to bf16 for P.V,
+// fp32 normaliser; see oracle/lm_oracle.py).
+//
+// MI355X design.  One workgroup = one (sequence, kv head, chunk of SPLIT positions); its
+// four waves are the four q heads of the GQA group.  Every K/V byte of the chunk is loaded
+// at kernel entry (one HBM round trip), parked in padded LDS tiles, and the math runs
+// lane-per-position (scores) and lane-per-dimension (P.V) out of LDS, so there are no
+// cross-lane shuffles: the softmax statistics use DPP reductions (VALU speed) instead of
+// __shfl_xor, which lowers to ds_bpermute and serialises on LDS latency.  Chunks of one
+// sequence are merged later (o_proj prologue or attn_combine_kernel).
+#include "hip_common.h"
+#include "lm_kernels.h"
+
+namespace tts {
+
+namespace {
+constexpr int G = 4;  // q heads per kv head = waves per workgroup
+
+template <int D>
+TTS_DEV float rope_at(const bf16_t* v, int d, const bf16_t* cosr, const bf16_t* sinr) {
+  constexpr int H2 = D / 2;
+  const float c = bf2f(cosr[d]), s = bf2f(sinr[d]);
+  const float x = bf2f(v[d]);
+  const float rot = (d < H2) ? -bf2f(v[d + H2]) : bf2f(v[d - H2]);
+  return rbf(rbf(x * c) + rbf(rot * s));
+}
+}  // namespace
+
+template <int D, int SPLIT>
+__global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
+  constexpr int KROW = D + 8;                 // bf16 row stride: 16-B pad, conflict-free b128
+  constexpr int CH = D / 8;                   // 16-B chunks per row
+  constexpr int LOADS = SPLIT * CH / 256;     // 16-B loads per thread per tile
+  constexpr int PPL = SPLIT / 64;             // positions per lane (scores)
+  constexpr int DPL = D / 64;                 // dims per lane (P.V)
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[SPLIT * KROW];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[SPLIT * KROW];
+  __shared__ __attribute__((aligned(16))) float qs[G * D];
+  __shared__ float ps[G * SPLIT];
+
+  const int nrk = a.rows * a.KVH, nb = nrk * a.nsplit;
+  if ((int)blockIdx.x >= nb) {  // cache-warming workgroups (next projections' weights)
+    prefetch_role(a.pf.ptr, a.pf.bytes, blockIdx.x - nb, gridDim.x - nb);
+    return;
+  }
+  const int rk = blockIdx.x % nrk, sp = blockIdx.x / nrk;
+  const int row = rk / a.KVH, kvh = rk % a.KVH;
+  const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
+  const int t0 = sp * SPLIT;
+  if (t0 >= ctx) return;
+  const int t1 = min(t0 + SPLIT, ctx);
+  const int n = t1 - t0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t cbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
+  const bf16_t* kc = a.kcache + cbase;
+  const bf16_t* vc = a.vcache + cbase;
+
+  // 1. the whole chunk's K and V in flight at once
+  u32x4_t kr[LOADS], vr[LOADS];
+#pragma unroll
+  for (int i = 0; i < LOADS; ++i) {
+    const int q = tid + i * 256, tl = q / CH, c = q % CH, t = t0 + tl;
+    if (t < t1 && t != pos) {
+      kr[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
+      vr[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
+    }
+  }
+  // 2. RoPE of the query heads; the new position's k (roped) and v go to the cache and LDS
+  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
+  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
+  const bf16_t* qrow = a.qkv + (size_t)row * a.ld_qkv;
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    qs[i] = rope_at<D>(qrow + (kvh * G + g) * D, d, cosr, sinr);
+  }
+  if (pos >= t0 && pos < t1) {
+    const bf16_t* kin = qrow + a.H * D + kvh * D;
+    const bf16_t* vin = kin + a.KVH * D;
+    for (int d = tid; d < D; d += 256) {
+      const bf16_t kb = f2bf(rope_at<D>(kin, d, cosr, sinr));
+      a.kcache[cbase + (size_t)pos * D + d] = kb;
+      a.vcache[cbase + (size_t)pos * D + d] = vin[d];
+      Ks[(pos - t0) * KROW + d] = kb;
+      Vs[(pos - t0) * KROW + d] = vin[d];
+    }
+  }
+  // 3. registers -> LDS tiles
+#pragma unroll
+  for (int i = 0; i < LOADS; ++i) {
+    const int q = tid + i * 256, tl = q / CH, c = q % CH, t = t0 + tl;
+    if (t < t1 && t != pos) {
+      *(u32x4_t*)(Ks + tl * KROW + c * 8) = kr[i];
+      *(u32x4_t*)(Vs + tl * KROW + c * 8) = vr[i];
+    }
+  }
+  __syncthreads();
+
+  // 4. scores: wave = q head, lane = position
+  const int g = wave;
+  const float* qg = qs + g * D;
+  float sc[PPL];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int tl = lane + 64 * j;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const u32x4_t kv = *(const u32x4_t*)(Ks + tl * KROW + c * 8);
+      const float4 q0 = *(const float4*)(qg + c * 8);
+      const float4 q1 = *(const float4*)(qg + c * 8 + 4);
+      acc += q0.x * bf_lo(kv[0]) + q0.y * bf_hi(kv[0]) + q0.z * bf_lo(kv[1]) + q0.w * bf_hi(kv[1]) +
+             q1.x * bf_lo(kv[2]) + q1.y * bf_hi(kv[2]) + q1.z * bf_lo(kv[3]) + q1.w * bf_hi(kv[3]);
+    }
+    sc[j] = (tl < n) ? acc * a.scale : -INFINITY;
+    mx = fmaxf(mx, sc[j]);
+  }
+  // 5. chunk softmax statistics (flash numerics: bf16 P for P.V, fp32 normaliser)
+  const float m = wave_max_dpp(mx);
+  float lsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const float p = (lane + 64 * j < n) ? expf(sc[j] - m) : 0.f;
+    lsum += p;
+    ps[g * SPLIT + lane + 64 * j] = rbf(p);
+  }
+  const float l = wave_sum_dpp(lsum);
+  __syncthreads();
+
+  // 6. P.V: wave = q head, lane = head dimension(s)
+  float o[DPL];
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) o[e] = 0.f;
+  const float* pg = ps + g * SPLIT;
+#pragma unroll 8
+  for (int tl = 0; tl < n; ++tl) {
+    const float p = pg[tl];
+    if constexpr (DPL == 1) {
+      o[0] += p * bf2f(Vs[tl * KROW + lane]);
+    } else {
+      const uint32_t v2 = *(const uint32_t*)(Vs + tl * KROW + 2 * lane);
+      o[0] += p * bf_lo(v2);
+      o[1] += p * bf_hi(v2);
+    }
+  }
+  const int h = kvh * G + g;
+  const size_t pidx = ((size_t)row * a.H + h) * a.nsplit + sp;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) a.part_o[pidx * D + lane * DPL + e] = o[e];
+  if (lane == 0) {
+    a.part_ml[pidx * 2] = m;
+    a.part_ml[pidx * 2 + 1] = l;
+  }
+}
+
+int decode_split(int D) { return D == 64 ? 128 : 64; }
+
+void launch_attn_decode_step(const AttnArgs& a, hipStream_t s) {
+  dim3 grid(a.rows * a.KVH * a.nsplit + ((a.pf.bytes && a.pf.ptr) ? a.pf.wgs : 0));
+  if (a.D == 64) hipLaunchKernelGGL((attn_decode2_kernel<64, 128>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((attn_decode2_kernel<128, 64>), grid, dim3(256), 0, s, a);
+}
+
+}  // namespace tts
