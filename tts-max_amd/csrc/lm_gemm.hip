@@ -111,12 +111,13 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 
   // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
   if constexpr (ASRC == A_LDS) {
-    for (int m = 0; m < M; ++m) {
+    // rows in parallel: wave w stages rows w, w+WAVES, ... (DPP row reduction, no barrier)
+    for (int m = wave; m < M; m += WAVES) {
       const bf16_t* xr = a.x + (size_t)m * a.ldx;
       float r = 1.0f;
       if constexpr (NORM) {
         float ss = 0.f;
-        for (int k = threadIdx.x * 8; k < a.K; k += NT * 8) {
+        for (int k = lane * 8; k < a.K; k += 64 * 8) {
           const u32x4_t v = *(const u32x4_t*)(xr + k);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -124,10 +125,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             ss += lo * lo + hi * hi;
           }
         }
-        ss = block_sum(ss, scal);
+        ss = wave_sum_dpp(ss);
         r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
       }
-      for (int k = threadIdx.x * 8; k < a.K; k += NT * 8) {
+      for (int k = lane * 8; k < a.K; k += 64 * 8) {
         u32x4_t v = *(const u32x4_t*)(xr + k);
         if constexpr (NORM) {
           const u32x4_t g = *(const u32x4_t*)(a.normw + k);
@@ -164,15 +165,25 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int s = 0; s < ns; ++s) fac[mh * NS + s] *= il;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < M * a.K; e += NT) {
-      const int m = e / a.K, hd = e % a.K, mh = m * H + hd / D, d = hd % D;
+    // 8 consecutive dims per thread: two float4 loads per chunk, one 16-B LDS store
+    for (int e = threadIdx.x; e < M * a.K / 8; e += NT) {
+      const int m = (e * 8) / a.K, hd = (e * 8) % a.K, mh = m * H + hd / D, d = hd % D;
       const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
       const float* po = a.attn_o + (size_t)mh * NS * D + d;
       const float* f = fac + mh * NS;
-      float o = 0.f;
+      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-      for (int s = 0; s < ns; ++s) o += po[(size_t)s * D] * f[s];
-      xs[(size_t)m * ldxs + hd] = f2bf(o);
+      for (int s = 0; s < ns; ++s) {
+        const float4 v0 = *(const float4*)(po + (size_t)s * D);
+        const float4 v1 = *(const float4*)(po + (size_t)s * D + 4);
+        const float fs = f[s];
+        o[0] += v0.x * fs; o[1] += v0.y * fs; o[2] += v0.z * fs; o[3] += v0.w * fs;
+        o[4] += v1.x * fs; o[5] += v1.y * fs; o[6] += v1.z * fs; o[7] += v1.w * fs;
+      }
+      u32x4_t pk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
+      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
     }
     __syncthreads();
   }
