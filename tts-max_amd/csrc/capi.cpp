@@ -201,7 +201,8 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, dev));
     WgemmPlan p = plan_wgemm(M, N, K, epi, prop.multiProcessorCount);
-    TTS_REQUIRE(normw == nullptr || p.a_lds, "fused RMSNorm needs M*K small enough for LDS");
+    TTS_REQUIRE(normw == nullptr || (p.a_lds && K <= 4096),
+                "fused RMSNorm needs M*K small enough for LDS and K <= 4096");
     WgemmArgs a;
     a.x = (const bf16_t*)x; a.M = M; a.K = K; a.ldx = ldx;
     a.w = (const bf16_t*)w_tiled; a.N = N;

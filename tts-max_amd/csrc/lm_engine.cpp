@@ -276,7 +276,7 @@ struct Ctx {
       WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
       const bf16_t* xin = x ? x + (size_t)r0 * K : nullptr;
       bool norm = normw != nullptr;
-      if (norm && !p.a_lds) {  // fused RMSNorm needs the rows in LDS: normalise separately
+      if (norm && (!p.a_lds || K > 4096)) {  // fused RMSNorm: rows in LDS, K <= 4096
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;

@@ -112,34 +112,51 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
   if constexpr (ASRC == A_LDS) {
     // rows in parallel: wave w stages rows w, w+WAVES, ... (DPP row reduction, no barrier)
+    // One pass per row, all of a lane's 16-B chunks in flight at once (K <= 4096 for the
+    // RMSNorm'ed rows; longer plain rows go in batches of 8 chunks).
+    constexpr int CPL = 8;  // chunks per lane held in registers
     for (int m = wave; m < M; m += WAVES) {
       const bf16_t* xr = a.x + (size_t)m * a.ldx;
-      float r = 1.0f;
-      if constexpr (NORM) {
-        float ss = 0.f;
-        for (int k = lane * 8; k < a.K; k += 64 * 8) {
-          const u32x4_t v = *(const u32x4_t*)(xr + k);
+      for (int k0 = 0; k0 < a.K; k0 += 64 * 8 * CPL) {
+        u32x4_t xv[CPL];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = bf_lo(v[q]), hi = bf_hi(v[q]);
-            ss += lo * lo + hi * hi;
+        for (int c = 0; c < CPL; ++c) {
+          const int k = k0 + (c * 64 + lane) * 8;
+          if (k < a.K) xv[c] = *(const u32x4_t*)(xr + k);
+        }
+        if constexpr (NORM) {  // (K <= 64*8*CPL: the whole row is in xv)
+          float ss = 0.f;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            if ((c * 64 + lane) * 8 < a.K) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float lo = bf_lo(xv[c][q]), hi = bf_hi(xv[c][q]);
+                ss += lo * lo + hi * hi;
+              }
+            }
+          }
+          ss = wave_sum_dpp(ss);
+          const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const int k = (c * 64 + lane) * 8;
+            if (k < a.K) {
+              const u32x4_t g = *(const u32x4_t*)(a.normw + k);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float lo = rbf(bf_lo(g[q]) * rbf(bf_lo(xv[c][q]) * r));
+                const float hi = rbf(bf_hi(g[q]) * rbf(bf_hi(xv[c][q]) * r));
+                xv[c][q] = pack_bf2(lo, hi);
+              }
+            }
           }
         }
-        ss = wave_sum_dpp(ss);
-        r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-      }
-      for (int k = lane * 8; k < a.K; k += 64 * 8) {
-        u32x4_t v = *(const u32x4_t*)(xr + k);
-        if constexpr (NORM) {
-          const u32x4_t g = *(const u32x4_t*)(a.normw + k);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r));
-            const float hi = rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r));
-            v[q] = pack_bf2(lo, hi);
-          }
+        for (int c = 0; c < CPL; ++c) {
+          const int k = k0 + (c * 64 + lane) * 8;
+          if (k < a.K) *(u32x4_t*)(xs + (size_t)m * ldxs + k) = xv[c];
         }
-        *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v;
       }
     }
     __syncthreads();
