@@ -40,9 +40,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
   const int arow = t / (GBK / (4 * AV)), ak = (t % (GBK / (4 * AV))) * 4 * AV;
   const int brow = t / (GBK / (4 * BV)), bk = (t % (GBK / (4 * BV))) * 4 * BV;
   const int ar = m0 + arow, br = n0 + brow;
-  const float* ap = g.A + (size_t)ar * g.lda + ak;
-  const float* bp = g.B + (size_t)br * g.K + bk;
   const bool aok = ar < g.M, bok = br < g.N;
+  // out-of-range rows read a clamped (valid) row and are zeroed after the load: a load
+  // inside a branch makes hipcc wait on it before the next one is issued
+  const float* ap = g.A + (size_t)(aok ? ar : g.M - 1) * g.lda + ak;
+  const float* bp = g.B + (size_t)(bok ? br : g.N - 1) * g.K + bk;
   f32x16_t acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -54,9 +56,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 ra[AV], rb[BV];
 #pragma unroll
-  for (int v = 0; v < AV; ++v) ra[v] = aok ? *(const float4*)(ap + 4 * v) : z4;
+  for (int v = 0; v < AV; ++v) {
+    const float4 l = *(const float4*)(ap + 4 * v);
+    ra[v] = aok ? l : z4;
+  }
 #pragma unroll
-  for (int v = 0; v < BV; ++v) rb[v] = bok ? *(const float4*)(bp + 4 * v) : z4;
+  for (int v = 0; v < BV; ++v) {
+    const float4 l = *(const float4*)(bp + 4 * v);
+    rb[v] = bok ? l : z4;
+  }
   for (int k0 = 0; k0 < g.K; k0 += GBK) {
     __syncthreads();
 #pragma unroll
@@ -77,9 +85,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
     if (k0 + GBK < g.K) {  // prefetch next K tile while the MFMAs run
       const int kn = k0 + GBK;
 #pragma unroll
-      for (int v = 0; v < AV; ++v) ra[v] = aok ? *(const float4*)(ap + kn + 4 * v) : z4;
+      for (int v = 0; v < AV; ++v) {
+        const float4 l = *(const float4*)(ap + kn + 4 * v);
+        ra[v] = aok ? l : z4;
+      }
 #pragma unroll
-      for (int v = 0; v < BV; ++v) rb[v] = bok ? *(const float4*)(bp + kn + 4 * v) : z4;
+      for (int v = 0; v < BV; ++v) {
+        const float4 l = *(const float4*)(bp + kn + 4 * v);
+        rb[v] = bok ? l : z4;
+      }
     }
 #pragma unroll
     for (int kk = 0; kk < GBK / 2; ++kk) {

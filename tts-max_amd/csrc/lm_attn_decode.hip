@@ -63,12 +63,11 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
   // 1. the whole chunk's K and V in flight at once
   u32x4_t kr[LOADS], vr[LOADS];
 #pragma unroll
-  for (int i = 0; i < LOADS; ++i) {
-    const int q = tid + i * 256, tl = q / CH, c = q % CH, t = t0 + tl;
-    if (t < t1 && t != pos) {
-      kr[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
-      vr[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
-    }
+  for (int i = 0; i < LOADS; ++i) {  // unconditional (clamped row): no branch around loads
+    const int q = tid + i * 256, tl = q / CH, c = q % CH;
+    const int t = (t0 + tl < t1) ? t0 + tl : t0;
+    kr[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
+    vr[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
   }
   // 2. RoPE of the query heads; the new position's k (roped) and v go to the cache and LDS
   const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
