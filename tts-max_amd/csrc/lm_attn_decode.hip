@@ -21,14 +21,6 @@ namespace tts {
 namespace {
 constexpr int G = 4;  // q heads per kv head = waves per workgroup
 
-template <int D>
-TTS_DEV float rope_at(const bf16_t* v, int d, const bf16_t* cosr, const bf16_t* sinr) {
-  constexpr int H2 = D / 2;
-  const float c = bf2f(cosr[d]), s = bf2f(sinr[d]);
-  const float x = bf2f(v[d]);
-  const float rot = (d < H2) ? -bf2f(v[d + H2]) : bf2f(v[d - H2]);
-  return rbf(rbf(x * c) + rbf(rot * s));
-}
 }  // namespace
 
 template <int D, int SPLIT>
@@ -60,41 +52,58 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
   const bf16_t* kc = a.kcache + cbase;
   const bf16_t* vc = a.vcache + cbase;
 
-  // 1. the whole chunk's K and V in flight at once
-  u32x4_t kr[LOADS], vr[LOADS];
+  // 1. RoPE operands first, then the whole chunk's K and V: vmcnt retires in issue order,
+  //    so the rotation below waits only for its own operands, not for the K/V stream.
+  constexpr int QPT = G * D / 256;  // query elements per thread
+  constexpr int H2 = D / 2;
+  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
+  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
+  const bf16_t* qrow = a.qkv + (size_t)row * a.ld_qkv;
+  const bf16_t* kin = qrow + a.H * D + kvh * D;
+  const bf16_t* vin = kin + a.KVH * D;
+  bf16_t qx[QPT], qr[QPT], qc[QPT], qsn[QPT];
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int i = tid + 256 * j, g = i / D, d = i % D;
+    const bf16_t* v = qrow + (kvh * G + g) * D;
+    qx[j] = v[d];
+    qr[j] = v[d < H2 ? d + H2 : d - H2];
+    qc[j] = cosr[d];
+    qsn[j] = sinr[d];
+  }
+  const int dk = tid % D;  // new-position k/v element of this thread (used by tid < D)
+  const bf16_t kx = kin[dk], kr = kin[dk < H2 ? dk + H2 : dk - H2], vx = vin[dk];
+  u32x4_t kr4[LOADS], vr4[LOADS];
 #pragma unroll
   for (int i = 0; i < LOADS; ++i) {  // unconditional (clamped row): no branch around loads
     const int q = tid + i * 256, tl = q / CH, c = q % CH;
     const int t = (t0 + tl < t1) ? t0 + tl : t0;
-    kr[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
-    vr[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
+    kr4[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
+    vr4[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
   }
-  // 2. RoPE of the query heads; the new position's k (roped) and v go to the cache and LDS
-  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
-  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
-  const bf16_t* qrow = a.qkv + (size_t)row * a.ld_qkv;
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, d = i % D;
-    qs[i] = rope_at<D>(qrow + (kvh * G + g) * D, d, cosr, sinr);
+  // 2. RoPE (HF apply_rotary_pos_emb in bf16: q*cos + rotate_half(q)*sin, each op rounded)
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int i = tid + 256 * j, d = i % D;
+    const float rot = (d < H2) ? -bf2f(qr[j]) : bf2f(qr[j]);
+    qs[i] = rbf(rbf(bf2f(qx[j]) * bf2f(qc[j])) + rbf(rot * bf2f(qsn[j])));
   }
-  if (pos >= t0 && pos < t1) {
-    const bf16_t* kin = qrow + a.H * D + kvh * D;
-    const bf16_t* vin = kin + a.KVH * D;
-    for (int d = tid; d < D; d += 256) {
-      const bf16_t kb = f2bf(rope_at<D>(kin, d, cosr, sinr));
-      a.kcache[cbase + (size_t)pos * D + d] = kb;
-      a.vcache[cbase + (size_t)pos * D + d] = vin[d];
-      Ks[(pos - t0) * KROW + d] = kb;
-      Vs[(pos - t0) * KROW + d] = vin[d];
-    }
+  if (pos >= t0 && pos < t1 && tid < D) {  // the new position: roped k and v to cache + LDS
+    const float c = bf2f(qc[0]), sn = bf2f(qsn[0]);  // (tid < D: element 0 is dimension dk)
+    const float rot = (dk < H2) ? -bf2f(kr) : bf2f(kr);
+    const bf16_t kb = f2bf(rbf(rbf(bf2f(kx) * c) + rbf(rot * sn)));
+    a.kcache[cbase + (size_t)pos * D + dk] = kb;
+    a.vcache[cbase + (size_t)pos * D + dk] = vx;
+    Ks[(pos - t0) * KROW + dk] = kb;
+    Vs[(pos - t0) * KROW + dk] = vx;
   }
   // 3. registers -> LDS tiles
 #pragma unroll
   for (int i = 0; i < LOADS; ++i) {
     const int q = tid + i * 256, tl = q / CH, c = q % CH, t = t0 + tl;
     if (t < t1 && t != pos) {
-      *(u32x4_t*)(Ks + tl * KROW + c * 8) = kr[i];
-      *(u32x4_t*)(Vs + tl * KROW + c * 8) = vr[i];
+      *(u32x4_t*)(Ks + tl * KROW + c * 8) = kr4[i];
+      *(u32x4_t*)(Vs + tl * KROW + c * 8) = vr4[i];
     }
   }
   __syncthreads();

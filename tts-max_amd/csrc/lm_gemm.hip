@@ -120,9 +120,9 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int k0 = 0; k0 < a.K; k0 += 64 * 8 * CPL) {
         u32x4_t xv[CPL];
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {  // clamped, unconditional: all chunks in flight
+        for (int c = 0; c < CPL; ++c) {
           const int k = k0 + (c * 64 + lane) * 8;
-          xv[c] = *(const u32x4_t*)(xr + (k < a.K ? k : a.K - 8));
+          if (k < a.K) xv[c] = *(const u32x4_t*)(xr + k);
         }
         if constexpr (NORM) {  // (K <= 64*8*CPL: the whole row is in xv)
           float ss = 0.f;
@@ -138,17 +138,11 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           }
           ss = wave_sum_dpp(ss);
           const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-          u32x4_t gv[CPL];
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            const int k = (c * 64 + lane) * 8;
-            gv[c] = *(const u32x4_t*)(a.normw + (k < a.K ? k : a.K - 8));
-          }
 #pragma unroll
           for (int c = 0; c < CPL; ++c) {
             const int k = (c * 64 + lane) * 8;
             if (k < a.K) {
-              const u32x4_t g = gv[c];
+              const u32x4_t g = *(const u32x4_t*)(a.normw + k);
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
                 const float lo = rbf(bf_lo(g[q]) * rbf(bf_lo(xv[c][q]) * r));
@@ -235,17 +229,16 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       const int unext = u + ustride;
       for (int kt = kt0; kt < kend; kt += KU) {
         // next stage: same unit, else the first stage of the wave's next unit
-        // (no next stage: every wave reads unit 0's first stage, which the whole grid shares
-        //  through L2, instead of HBM; the loads stay unconditional because hipcc waits
-        //  vmcnt(0) around loads it has to branch over)
         int nu = u, nk = kt + KU;
         if (nk >= kend) { nu = unext; nk = kt0; }
-        if (nu >= units) { nu = 0; nk = 0; }
+        const bool has_next = nu < units;
         u32x4_t wn[KU][NG];
+        if (has_next) {
 #pragma unroll
-        for (int kk = 0; kk < KU; ++kk)
+          for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
-          for (int g = 0; g < NG; ++g) wn[kk][g] = __builtin_nontemporal_load(wptr(nu, g) + (nk + kk) * 64);
+            for (int g = 0; g < NG; ++g) wn[kk][g] = __builtin_nontemporal_load(wptr(nu, g) + (nk + kk) * 64);
+        }
 
 #pragma unroll
         for (int kk = 0; kk < KU; ++kk) {
@@ -254,13 +247,11 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           for (int mt = 0; mt < MT_MAX; ++mt) {
             if (mt < mtn) {
               const int m = mt * 16 + arow;
-              // unconditional read of a valid row, zeroed by select (no branch around a load)
-              const int mc = m < M ? m : M - 1;
-              u32x4_t av;
-              if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)mc * ldxs + k);
-              else av = *(const u32x4_t*)(a.x + (size_t)mc * a.ldx + k);
-              const u32x4_t zero = u32x4_t{0u, 0u, 0u, 0u};
-              av = (m < M) ? av : zero;
+              u32x4_t av = u32x4_t{0u, 0u, 0u, 0u};
+              if (m < M) {
+                if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
+                else av = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+              }
               const bf16x8_t af = as_bf16x8(av);
 #pragma unroll
               for (int g = 0; g < NG; ++g)
@@ -269,10 +260,12 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             }
           }
         }
+        if (has_next) {
 #pragma unroll
-        for (int kk = 0; kk < KU; ++kk)
+          for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
-          for (int g = 0; g < NG; ++g) wb[kk][g] = wn[kk][g];
+            for (int g = 0; g < NG; ++g) wb[kk][g] = wn[kk][g];
+        }
       }
     }
 

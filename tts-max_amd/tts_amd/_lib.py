@@ -18,7 +18,8 @@ import os
 import torch  # noqa: F401  (must load the HIP runtime before the library; see docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtts_mi355x.so")
+# TTS_LIB_PATH: load another build of the same library (A/B experiments, scripts/ab_*.sh)
+LIB_PATH = os.environ.get("TTS_LIB_PATH") or os.path.join(_HERE, "libtts_mi355x.so")
 
 TTS_OK = 0
 DT_F32, DT_BF16, DT_F16, DT_I32, DT_I64 = 0, 1, 2, 3, 4
