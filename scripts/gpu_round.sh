@@ -17,11 +17,11 @@ for step in "$@"; do
       timeout -k 10 900 python bench.py > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err; rc=$?
       tail -3 $OUT/${TAG}_bench.err; cat $OUT/${TAG}_bench.json; stop_if_fatal $rc bench ;;
     bench32)
-      timeout -k 10 900 python bench.py --batch 32 --no-cpu-baseline --no-pmc > $OUT/${TAG}_bench32.json 2> $OUT/${TAG}_bench32.err; rc=$?
+      timeout -k 10 900 python bench.py --batch 32 --no-cpu-baseline > $OUT/${TAG}_bench32.json 2> $OUT/${TAG}_bench32.err; rc=$?
       tail -3 $OUT/${TAG}_bench32.err; cat $OUT/${TAG}_bench32.json; stop_if_fatal $rc bench32 ;;
     prof)
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o run -- \
-        python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pmc > $OUT/${TAG}_prof.log 2>&1; rc=$?
+        python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/${TAG}_prof.log 2>&1; rc=$?
       tail -3 $OUT/${TAG}_prof.log; find $OUT/${TAG}_prof -name "*stats*"; stop_if_fatal $rc prof ;;
   esac
 done
