@@ -19,6 +19,8 @@
 // and tiles of one n-tile are consecutive along K.  Activations (M <= 64 rows) are the
 // A operand; at M = 1 fifteen of the sixteen A rows are zero, which costs nothing because
 // the kernel is HBM-bound on the weight stream.
+#include <algorithm>
+
 #include "hip_common.h"
 #include "lm_kernels.h"
 
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     return;
   }
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kpart = wave % KSPLIT;
   const int ugrp = wave / KSPLIT;
   const int M = a.M;
@@ -94,10 +96,84 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   bf16_t* xs = (bf16_t*)smem;
   const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
   float* red = (float*)(smem + xs_bytes);  // [WAVES][NG*MT_MAX*4][64] split-K partials
-  float* scal = red + WAVES * NG * MT_MAX * 4 * 64;
+  float* xtra = red + WAVES * NG * MT_MAX * 4 * 64 + 64;  // A_ATTN scratch
 
-  // ---- start the weight stream before anything else
+  // ---- operands of the prologue and epilogue are loaded FIRST, the weight stream after:
+  // vmcnt retires in issue order, so anything issued behind the stream could not be used
+  // before the whole first weight stage had landed.
+  const int tid = threadIdx.x;
+  const int kch = a.K >> 3;  // 16-B chunks per A row
+  // (a) A rows (+ RMSNorm weight) for the LDS prologue, EA chunks per thread at most
+  constexpr int EA = 4;
+  const int achunks = M * kch;
+  const int a_nj = (achunks + NT - 1) / NT;
+  const bool early_a = (ASRC == A_LDS) && a_nj <= EA && (kch & 63) == 0;
+  u32x4_t xe[EA], ne[EA];
+  if constexpr (ASRC == A_LDS) {
+    if (early_a) {
+#pragma unroll
+      for (int j = 0; j < EA; ++j) {
+        if (j < a_nj) {  // uniform
+          const int c = min(tid + j * NT, achunks - 1);
+          const int m = c / kch, k = (c - m * kch) * 8;
+          xe[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+          if constexpr (NORM) ne[j] = *(const u32x4_t*)(a.normw + k);
+        }
+      }
+    }
+  }
+  // (b) attention chunk partials for the o_proj prologue: thread = (row, 8 dims) item x
+  //     chunk group; every chunk statistic of the item's head, CPG chunk vectors
+  constexpr int NSX = 8, CPG = (WAVES >= 16) ? 2 : 4;
+  const int NS = a.attn_nsplit;
+  const int aitems = M * kch;
+  const int agroups = (ASRC == A_ATTN && aitems <= NT) ? NT / aitems : 0;
+  const int acpg = agroups ? (NS + agroups - 1) / agroups : CPG + 1;
+  const bool early_o = (ASRC == A_ATTN) && agroups > 0 && NS <= NSX && acpg <= CPG;
+  float2 mle[NSX], mlo[CPG];
+  float4 poe[CPG][2];
+  int pose = 0;
+  if constexpr (ASRC == A_ATTN) {
+    if (early_o) {
+      const int it = tid % aitems, grp = min(tid / aitems, agroups - 1);
+      const int D = a.attn_D, H = a.K / D;
+      const int m = it / kch, hd = (it - m * kch) * 8;
+      const size_t mh = (size_t)m * H + hd / D;
+      const int d = hd % D;
+      pose = a.attn_pos[m];
+#pragma unroll
+      for (int s = 0; s < NSX; ++s) mle[s] = *(const float2*)(a.attn_ml + (mh * NS + min(s, NS - 1)) * 2);
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const int s = min(grp * acpg + i, NS - 1);
+        const float* po = a.attn_o + (mh * NS + s) * D + d;
+        poe[i][0] = *(const float4*)po;
+        poe[i][1] = *(const float4*)(po + 4);
+        mlo[i] = *(const float2*)(a.attn_ml + (mh * NS + s) * 2);
+      }
+    }
+  }
+  // (c) epilogue operands of the wave's first unit: residual values / EOS mask + seen bits
   int u = blockIdx.x * UPW + ugrp;
+  const int u_first = min(u, units - 1);
+  bf16_t rre[MT_MAX][4];
+  int eosr[MT_MAX][4];
+  uint32_t seen_cur[MT_MAX][4];
+#pragma unroll
+  for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (mt < mtn) {
+        const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
+        if constexpr (EPI == EPI_RESID) rre[mt][r] = a.resid[(size_t)m * a.ldo + u_first * 16 + (lane & 15)];
+        if constexpr (EPI == EPI_LOGITS) {
+          eosr[mt][r] = a.eos_mask[m];
+          seen_cur[mt][r] = a.seen[(size_t)m * a.seen_stride + (u_first >> 1)];
+        }
+      }
+    }
+
+  // ---- then the weight stream
   u32x4_t wb[KU][NG];
   auto wptr = [&](int uu, int g) {
     return (const u32x4_t*)(a.w + ((size_t)(uu * NG + g) * KT) * 512) + lane;
@@ -111,6 +187,51 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 
   // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
   if constexpr (ASRC == A_LDS) {
+   if (early_a) {
+    // rows already in registers: RMSNorm statistics per 64-chunk wave segment (DPP), the
+    // segments of a row summed in fixed order after one barrier
+    if constexpr (NORM) {
+#pragma unroll
+      for (int j = 0; j < EA; ++j) {
+        if (j < a_nj) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = bf_lo(xe[j][q]), hi = bf_hi(xe[j][q]);
+            s += lo * lo + hi * hi;
+          }
+          s = wave_sum_dpp(s);
+          const int c = tid + j * NT;
+          if (lane == 0 && c < achunks) red[c >> 6] = s;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < EA; ++j) {
+      if (j < a_nj) {
+        const int c = tid + j * NT;
+        if (c < achunks) {
+          const int m = c / kch, k = (c - m * kch) * 8;
+          u32x4_t v = xe[j];
+          if constexpr (NORM) {
+            const int seg0 = (m * kch) >> 6, nseg = kch >> 6;
+            float ss = 0.f;
+            for (int sg = 0; sg < nseg; ++sg) ss += red[seg0 + sg];
+            const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float lo = rbf(bf_lo(ne[j][q]) * rbf(bf_lo(v[q]) * r));
+              const float hi = rbf(bf_hi(ne[j][q]) * rbf(bf_hi(v[q]) * r));
+              v[q] = pack_bf2(lo, hi);
+            }
+          }
+          *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v;
+        }
+      }
+    }
+    __syncthreads();
+   } else {
     // rows in parallel: wave w stages rows w, w+WAVES, ... (DPP row reduction, no barrier)
     // One pass per row, all of a lane's 16-B chunks in flight at once (K <= 4096 for the
     // RMSNorm'ed rows; longer plain rows go in batches of 8 chunks).
@@ -160,12 +281,59 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
     __syncthreads();
+   }
   } else if constexpr (ASRC == A_ATTN) {
+   if (early_o) {
+    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
+    const int it = tid % aitems, grp = tid / aitems;
+    const int ns = (pose + a.attn_split) / a.attn_split;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < NSX; ++s) if (s < ns) mx = fmaxf(mx, mle[s].x);
+    float l = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSX; ++s) if (s < ns) l += mle[s].y * expf(mle[s].x - mx);
+    const float il = 1.0f / l;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < CPG; ++i) {
+      const int s = grp * acpg + i;
+      if (i < acpg && s < ns) {
+        const float fs = expf(mlo[i].x - mx) * il;
+        o[0] += poe[i][0].x * fs; o[1] += poe[i][0].y * fs; o[2] += poe[i][0].z * fs; o[3] += poe[i][0].w * fs;
+        o[4] += poe[i][1].x * fs; o[5] += poe[i][1].y * fs; o[6] += poe[i][1].z * fs; o[7] += poe[i][1].w * fs;
+      }
+    }
+    const int m = it / kch, hd = (it - m * kch) * 8;
+    if (agroups > 1) {  // chunk groups of an item summed in fixed order through LDS
+      if (grp < agroups) {
+        float4* op = (float4*)xtra + (size_t)(grp * aitems + it) * 2;
+        op[0] = make_float4(o[0], o[1], o[2], o[3]);
+        op[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
+      __syncthreads();
+      if (grp == 0) {
+        for (int g = 1; g < agroups; ++g) {
+          const float4* op = (const float4*)xtra + (size_t)(g * aitems + it) * 2;
+          const float4 v0 = op[0], v1 = op[1];
+          o[0] += v0.x; o[1] += v0.y; o[2] += v0.z; o[3] += v0.w;
+          o[4] += v1.x; o[5] += v1.y; o[6] += v1.z; o[7] += v1.w;
+        }
+      }
+    }
+    if (grp == 0) {
+      u32x4_t pk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
+      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
+    }
+    __syncthreads();
+   } else {
     // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
     // phase 1: one thread per (row, head) turns the chunk statistics into factors (LDS);
     // phase 2: every thread merges its (row, head, dim) elements with independent loads.
     const int D = a.attn_D, H = a.K / D, NS = a.attn_nsplit;
-    float* fac = (float*)(smem + xs_bytes) + WAVES * NG * MT_MAX * 4 * 64 + 64;
+    float* fac = xtra;
     for (int mh = threadIdx.x; mh < M * H; mh += NT) {
       const int m = mh / H;
       const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
@@ -203,6 +371,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
     }
     __syncthreads();
+   }
   }
 
   const int arow = lane & 15;
@@ -216,9 +385,22 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { best_v[mt][r] = -INFINITY; best_i[mt][r] = 0x7fffffff; }
 
+  bool first = true;
   for (int ubase = blockIdx.x * UPW; ubase < units; ubase += ustride) {
     u = ubase + ugrp;
     const bool active = u < units;
+    uint32_t seen_nxt[MT_MAX][4];
+    if constexpr (EPI == EPI_LOGITS) {  // next unit's penalty bits, in flight with this unit
+      const int un = min(u + ustride, units - 1);
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (mt < mtn) {
+            const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
+            seen_nxt[mt][r] = a.seen[(size_t)m * a.seen_stride + (un >> 1)];
+          }
+    }
     f32x4_t acc[NG][MT_MAX];
 #pragma unroll
     for (int g = 0; g < NG; ++g)
@@ -313,7 +495,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
           } else if constexpr (EPI == EPI_RESID) {
             bf16_t* p = a.resid + (size_t)m * a.ldo + n;
-            *p = f2bf(bf2f(*p) + rbf(acc[0][mt][r]));
+            *p = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
           } else if constexpr (EPI == EPI_SWIGLU) {
             // unit u = (gate tile, up tile) pair for intermediate columns u*16 .. u*16+15
             const float gt = rbf(acc[0][mt][r]);
@@ -321,13 +503,20 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             a.out[(size_t)m * a.ldo + n] = f2bf(rbf(silu_f(gt)) * up);
           } else if constexpr (EPI == EPI_LOGITS) {
             float v = rbf(acc[0][mt][r]);  // logits are materialised in bf16, then .float()
-            const uint32_t bits = a.seen[(size_t)m * a.seen_stride + (n >> 5)];
+            const uint32_t bits = seen_cur[mt][r];
             if ((bits >> (n & 31)) & 1u) v = (v < 0.f) ? v * a.penalty : v / a.penalty;
-            if (n == a.eos_mask[m]) v = -INFINITY;
+            if (n == eosr[mt][r]) v = -INFINITY;
             argmax_merge(best_v[mt][r], best_i[mt][r], v, n);
           }
         }
       }
+    }
+    first = false;
+    if constexpr (EPI == EPI_LOGITS) {
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) seen_cur[mt][r] = seen_nxt[mt][r];
     }
   }
 
@@ -377,7 +566,8 @@ static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
   const int mt = a.M <= 16 ? 1 : 4;
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
   lds += (size_t)(WAVES * NG * mt * 4 * 64 + 64) * sizeof(float);
-  if (ASRC == A_ATTN) lds += (size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit * sizeof(float);
+  if (ASRC == A_ATTN)  // chunk factors (fallback path) or chunk-group partials (early path)
+    lds += std::max((size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit, (size_t)WAVES * 64 * 8) * sizeof(float);
   if (mt == 1) {
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
                        dim3(WAVES * 64), lds, s, a);
