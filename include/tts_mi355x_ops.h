@@ -20,8 +20,10 @@ extern "C" {
 tts_status tts_synth_fill(void* dst, int32_t dtype, int64_t n, uint64_t seed, float scale,
                           void* stream);
 
-/* W [N][K] bf16 row-major -> 1 KiB MFMA fragment tiles (layout in lm_gemm.hip). */
-tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, void* stream);
+/* W [N][K] bf16 row-major -> 1 KiB MFMA fragment tiles in the matrix's stream-plan order
+ * (layout in lm_kernels.h / lm_gemm.hip).  epi = the epilogue the matrix will be used with:
+ * 2 (SwiGLU) takes W = [gate; up] ([N/2][K] each) and interleaves their n-tiles. */
+tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, int32_t epi, void* stream);
 
 /* y[M][ldo] (bf16) = epilogue( A[M][K] . W^T ), A optionally RMSNorm'ed with normw.
  * epi: 0 store, 1 residual (resid += y, in place), 2 SwiGLU (W = interleaved gate/up tiles,

@@ -1,0 +1,156 @@
+// hbm_floor.hip — what does a plain streaming read of B bytes cost per launch on this GPU?
+// The floor the decode-step weight-streaming kernels are measured against: a grid-stride
+// read of the decode GEMV sizes (8.4 / 12.6 / 33.5 / 67 / 794 MB), back-to-back launches
+// rotating over > 600 MB of buffers (HBM-cold, as in the decode step), per launch shape.
+// build: hipcc -O3 --offload-arch=gfx950 scripts/hbm_floor.hip -o scripts/hbm_floor
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+template <int LPT, bool NT>
+__global__ void stream_kernel(const u32x4_t* __restrict__ p, size_t n16, unsigned* sink) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  u32x4_t acc = {0u, 0u, 0u, 0u};
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += LPT * stride) {
+    u32x4_t v[LPT];
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+      const size_t k = i + j * stride;
+      const size_t kk = k < n16 ? k : i;
+      v[j] = NT ? __builtin_nontemporal_load(p + kk) : p[kk];
+    }
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) acc ^= v[j];
+  }
+  if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x12345678u) sink[0] = 1;
+}
+
+
+// The GEMV kernels' pattern: each wave streams its own tiles (1 KiB per wave-instruction)
+// in stages of KU tiles, double-buffered (stage s+1 issued before stage s is consumed).
+// PAT 0: a wave's tiles contiguous; PAT 1: stage-interleaved (at stage s all waves read
+// one contiguous block).
+template <int KU, int PAT>
+__global__ void pipe_kernel(const u32x4_t* __restrict__ p, int tpw, unsigned* sink) {
+  const int lane = threadIdx.x & 63;
+  const int nwpb = blockDim.x >> 6;
+  const int gw = blockIdx.x * nwpb + (threadIdx.x >> 6);
+  const int nw = gridDim.x * nwpb;
+  auto tile = [&](int t) -> size_t {
+    if (PAT == 0) return (size_t)gw * tpw + t;
+    return ((size_t)(t / KU) * nw + gw) * KU + (t % KU);
+  };
+  u32x4_t acc = {0u, 0u, 0u, 0u};
+  u32x4_t wb[KU];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) wb[k] = __builtin_nontemporal_load(p + tile(k) * 64 + lane);
+  for (int t = 0; t < tpw; t += KU) {
+    u32x4_t wn[KU];
+    const bool nx = t + KU < tpw;
+    if (nx) {
+#pragma unroll
+      for (int k = 0; k < KU; ++k) wn[k] = __builtin_nontemporal_load(p + tile(t + KU + k) * 64 + lane);
+    }
+#pragma unroll
+    for (int k = 0; k < KU; ++k) acc ^= wb[k];
+    if (nx) {
+#pragma unroll
+      for (int k = 0; k < KU; ++k) wb[k] = wn[k];
+    }
+  }
+  if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x12345678u) sink[0] = 1;
+}
+
+int main() {
+  const double sizes_mb[] = {8.388608, 12.582912, 33.554432, 67.108864, 794.034176};
+  const size_t pool = (size_t)1600 << 20;
+  char* buf;
+  unsigned* sink;
+  hipMalloc(&buf, pool);
+  hipMalloc(&sink, 64);
+  hipMemset(buf, 1, pool);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (double mb : sizes_mb) {
+    const size_t bytes = (size_t)(mb * 1e6);
+    const size_t n16 = bytes / 16;
+    const int copies = (int)(pool / bytes) > 16 ? 16 : (int)(pool / bytes);
+    float best = 1e9f;
+    char bestcfg[64] = "";
+    for (int grid : {256, 512, 1024, 2048}) {
+      for (int threads : {256, 512, 1024}) {
+        for (int lpt : {4, 8, 16}) {
+          for (int nt = 0; nt < 2; ++nt) {
+            auto launch = [&](int c) {
+              const u32x4_t* p = (const u32x4_t*)(buf + (size_t)c * bytes);
+#define L(LP, N) hipLaunchKernelGGL((stream_kernel<LP, N>), dim3(grid), dim3(threads), 0, 0, p, n16, sink)
+              if (lpt == 4) { if (nt) L(4, true); else L(4, false); }
+              else if (lpt == 8) { if (nt) L(8, true); else L(8, false); }
+              else { if (nt) L(16, true); else L(16, false); }
+            };
+            const int iters = copies >= 2 ? 48 : 16;
+            for (int i = 0; i < 4; ++i) launch(i % copies);
+            hipEventRecord(a, 0);
+            for (int i = 0; i < iters; ++i) launch(i % copies);
+            hipEventRecord(b, 0);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            const float us = ms * 1000.f / iters;
+            if (us < best) {
+              best = us;
+              snprintf(bestcfg, sizeof bestcfg, "grid %d x %d thr, %d ld/thr, nt %d", grid, threads, lpt, nt);
+            }
+            if (grid == 1024 && threads == 256 && lpt == 8)
+              printf("  %8.1f MB  grid 1024x256 8ld nt%d: %8.2f us  %7.1f GB/s\n", mb, nt, us, bytes / us / 1e3);
+          }
+        }
+      }
+    }
+    printf("%8.1f MB  best %8.2f us  %7.1f GB/s  (%s)\n", mb, best, bytes / best / 1e3, bestcfg);
+    fflush(stdout);
+  }
+
+  // ---- pattern sweep
+  for (double mb : {12.582912, 67.108864, 794.034176}) {
+    const size_t bytes = (size_t)(mb * 1e6);
+    const size_t tiles = bytes / 1024;
+    const int copies = (int)(pool / bytes) > 16 ? 16 : (int)(pool / bytes);
+    for (int waves : {4, 8, 16}) {
+      for (int grid : {256, 512}) {
+        const int nw = grid * waves;
+        for (int ku : {2, 4, 8, 16}) {
+          if (tiles % ((size_t)nw * ku)) continue;
+          const int tpw = (int)(tiles / nw);
+          for (int pat = 0; pat < 2; ++pat) {
+            auto launch = [&](int c) {
+              const u32x4_t* p = (const u32x4_t*)(buf + (size_t)c * bytes);
+#define P(KU, PT) hipLaunchKernelGGL((pipe_kernel<KU, PT>), dim3(grid), dim3(waves * 64), 0, 0, p, tpw, sink)
+              if (ku == 2) { if (pat) P(2, 1); else P(2, 0); }
+              else if (ku == 4) { if (pat) P(4, 1); else P(4, 0); }
+              else if (ku == 8) { if (pat) P(8, 1); else P(8, 0); }
+              else { if (pat) P(16, 1); else P(16, 0); }
+            };
+            const int iters = copies >= 2 ? 48 : 16;
+            for (int i = 0; i < 4; ++i) launch(i % copies);
+            hipEventRecord(a, 0);
+            for (int i = 0; i < iters; ++i) launch(i % copies);
+            hipEventRecord(b, 0);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            const float us = ms * 1000.f / iters;
+            printf("pipe %7.1f MB waves %2d grid %3d KU %2d pat %d tpw %4d: %8.2f us %7.1f GB/s\n", mb, waves, grid,
+                   ku, pat, tpw, us, bytes / us / 1e3);
+          }
+        }
+      }
+    }
+    fflush(stdout);
+  }
+  return 0;
+}

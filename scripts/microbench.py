@@ -45,7 +45,7 @@ def main():
         for _ in range(R):
             w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
             wt = torch.empty_like(w)
-            _lib.check(lib.tts_op_retile(w.data_ptr(), wt.data_ptr(), N, K, stream))
+            _lib.check(lib.tts_op_retile(w.data_ptr(), wt.data_ptr(), N, K, 2 if name == "gate_up" else 0, stream))
             wts.append(wt)
             del w
         out = torch.empty(1, N if name != "gate_up" else N // 2, device=dev, dtype=torch.bfloat16)

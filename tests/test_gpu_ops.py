@@ -55,10 +55,10 @@ def test_synth_fill_bit_identical(lib):
         assert torch.equal(b.cpu(), torch.from_numpy(ref).to(torch.bfloat16))
 
 
-def _tiled(lib, w):
+def _tiled(lib, w, epi=0):
     N, K = w.shape
     t = torch.empty_like(w)
-    _check(lib.tts_op_retile(w.data_ptr(), t.data_ptr(), N, K, None))
+    _check(lib.tts_op_retile(w.data_ptr(), t.data_ptr(), N, K, epi, None))
     return t
 
 
@@ -88,9 +88,7 @@ def test_wgemm_norm_resid_swiglu(lib, M):
     h = lm_oracle.rmsnorm(x, nw, 1e-5)
     ref_act = torch.nn.functional.silu(lm_oracle.linear(h, wg)) * lm_oracle.linear(h, wu)
     # interleaved gate/up tiles, as the engine lays out mlp.gate_proj / mlp.up_proj
-    gt, ut = _tiled(lib, wg.cuda()), _tiled(lib, wu.cuda())
-    KT = K // 32
-    wgu = torch.stack([gt.view(FF // 16, KT * 512), ut.view(FF // 16, KT * 512)], 1).reshape(2 * FF, K).contiguous()
+    wgu = _tiled(lib, torch.cat([wg, wu]).cuda(), epi=2)
     out = torch.empty(M, FF, dtype=torch.bfloat16, device="cuda")
     xd, nd = x.cuda(), nw.cuda()
     _check(lib.tts_op_wgemm(xd.data_ptr(), M, K, K, wgu.data_ptr(), 2 * FF, nd.data_ptr(), 1e-5, out.data_ptr(), FF,

@@ -65,7 +65,6 @@ tts_status tts_engine_create(int32_t device, tts_engine** out) {
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     e->num_cu = prop.multiProcessorCount;
     HIP_CHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    if (const char* v = getenv("TTS_PREFETCH")) e->prefetch = atoi(v) != 0;
     for (auto& v : e->ev) HIP_CHECK(hipEventCreate(&v));
     *out = reinterpret_cast<tts_engine*>(e);
   });
@@ -181,10 +180,27 @@ tts_status tts_synth_fill(void* dst, int32_t dtype, int64_t n, uint64_t seed, fl
   });
 }
 
-tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, void* stream) {
+static int device_cu_count() {  // (single-device process: cached, no per-call query)
+  static int num_cu = 0;
+  if (!num_cu) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return num_cu;
+}
+
+tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, int32_t epi, void* stream) {
   return guarded([&] {
-    TTS_REQUIRE(w && w_tiled && N % 16 == 0 && K % 32 == 0, "bad argument");
-    launch_retile((const bf16_t*)w, (bf16_t*)w_tiled, N, K, (hipStream_t)stream, 1, 0);
+    TTS_REQUIRE(w && w_tiled && N % (epi == EPI_SWIGLU ? 32 : 16) == 0 && K % 256 == 0, "bad argument");
+    const int ncu = device_cu_count();
+    if (epi == EPI_SWIGLU) {  // rows [0, N/2) = gate, [N/2, N) = up: n-tiles interleaved
+      const bf16_t* wg = (const bf16_t*)w;
+      launch_retile(wg, (bf16_t*)w_tiled, N / 2, K, N, 2, ncu, (hipStream_t)stream, 2, 0);
+      launch_retile(wg + (size_t)(N / 2) * K, (bf16_t*)w_tiled, N / 2, K, N, 2, ncu, (hipStream_t)stream, 2, 1);
+    } else {
+      launch_retile((const bf16_t*)w, (bf16_t*)w_tiled, N, K, N, 1, ncu, (hipStream_t)stream, 1, 0);
+    }
     HIP_CHECK(hipGetLastError());
   });
 }
@@ -196,11 +212,7 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
     TTS_REQUIRE(epi == EPI_STORE || epi == EPI_RESID || epi == EPI_SWIGLU, "bad epilogue");
     TTS_REQUIRE(wgemm_supported(M, N, K, epi), "unsupported GEMM shape");
     TTS_REQUIRE(ldx == K, "ldx must equal K");
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    hipDeviceProp_t prop;
-    HIP_CHECK(hipGetDeviceProperties(&prop, dev));
-    WgemmPlan p = plan_wgemm(M, N, K, epi, prop.multiProcessorCount);
+    WgemmPlan p = plan_wgemm(M, N, K, epi, device_cu_count());
     TTS_REQUIRE(normw == nullptr || (p.a_lds && K <= 4096),
                 "fused RMSNorm needs M*K small enough for LDS and K <= 4096");
     WgemmArgs a;

@@ -111,10 +111,6 @@ struct Engine {
   Codec* codec = nullptr;
   float t_prefill_ms = 0.f, t_decode_ms = 0.f;
   int decode_steps = 0;
-  // decode-step cache warming by idle-CU workgroups (env TTS_PREFETCH=1 enables).  Off by
-  // default: measured slower (r1e A/B, profiles/): the warming reads compete with the
-  // latency-bound launches they were meant to hide behind.
-  bool prefetch = false;
   ~Engine();
 };
 

@@ -91,22 +91,3 @@ TTS_DEV float block_max(float v, float* red) {
 }
 
 TTS_DEV float silu_f(float x) { return x / (1.0f + expf(-x)); }
-
-// Cache-warming side role: workgroups appended to a latency-bound launch read a byte range
-// the NEXT launches will stream (the following projection's weights), so those reads
-// overlap this launch and the consumer finds the lines in the 256 MiB Infinity Cache.
-// Plain loads (not nt) so the lines are allocated; the values are consumed by an empty asm.
-TTS_DEV void prefetch_role(const void* p, size_t bytes, int wg, int nwg) {
-  const u32x4_t* q = (const u32x4_t*)p;
-  const size_t n16 = bytes / 16;
-  const size_t stride = (size_t)nwg * blockDim.x;
-  u32x4_t acc = u32x4_t{0u, 0u, 0u, 0u};
-  for (size_t i = (size_t)wg * blockDim.x + threadIdx.x; i < n16; i += 8 * stride) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const size_t k = i + j * stride;
-      if (k < n16) acc ^= q[k];
-    }
-  }
-  asm volatile("" ::"v"(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]));
-}

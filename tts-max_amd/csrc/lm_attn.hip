@@ -222,10 +222,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
   __shared__ float ml[2 * GQA];
   __shared__ float ored[4 * GQA * D];
   const int nrk = a.rows * a.KVH, nb = nrk * a.nsplit;
-  if ((int)blockIdx.x >= nb) {  // cache-warming workgroups (next projections' weights)
-    prefetch_role(a.pf.ptr, a.pf.bytes, blockIdx.x - nb, gridDim.x - nb);
-    return;
-  }
+  if ((int)blockIdx.x >= nb) return;
   const int rk = blockIdx.x % nrk, sp = blockIdx.x / nrk;
   const int row = rk / a.KVH, kvh = rk % a.KVH;
   const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
@@ -372,7 +369,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
 // (superseded by lm_attn_decode.hip: the lane-shuffle reductions above lower to
 //  ds_bpermute and serialise on LDS latency; kept only for reference / A-B runs)
 void launch_attn_decode_step_shfl(const AttnArgs& a, hipStream_t s) {
-  dim3 grid(a.rows * a.KVH * a.nsplit + ((a.pf.bytes && a.pf.ptr) ? a.pf.wgs : 0));
+  dim3 grid(a.rows * a.KVH * a.nsplit);
   if (a.D == 64) hipLaunchKernelGGL((attn_decode_kernel<64, 4>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((attn_decode_kernel<128, 4>), grid, dim3(256), 0, s, a);
 }

@@ -36,10 +36,7 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
   __shared__ float ps[G * SPLIT];
 
   const int nrk = a.rows * a.KVH, nb = nrk * a.nsplit;
-  if ((int)blockIdx.x >= nb) {  // cache-warming workgroups (next projections' weights)
-    prefetch_role(a.pf.ptr, a.pf.bytes, blockIdx.x - nb, gridDim.x - nb);
-    return;
-  }
+  if ((int)blockIdx.x >= nb) return;
   const int rk = blockIdx.x % nrk, sp = blockIdx.x / nrk;
   const int row = rk / a.KVH, kvh = rk % a.KVH;
   const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
@@ -169,7 +166,7 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
 int decode_split(int D) { return D == 64 ? 128 : 64; }
 
 void launch_attn_decode_step(const AttnArgs& a, hipStream_t s) {
-  dim3 grid(a.rows * a.KVH * a.nsplit + ((a.pf.bytes && a.pf.ptr) ? a.pf.wgs : 0));
+  dim3 grid(a.rows * a.KVH * a.nsplit);
   if (a.D == 64) hipLaunchKernelGGL((attn_decode2_kernel<64, 128>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((attn_decode2_kernel<128, 64>), grid, dim3(256), 0, s, a);
 }

@@ -166,35 +166,37 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
 
   DevBuf staging, staging32;
   staging.alloc((size_t)std::max<size_t>((size_t)V * HID, (size_t)FF * HID) * 2);
-  auto retiled = [&](const tts_tensor_desc& d, bf16_t* dst, int N, int K, int mult, int off) {
+  // matrix (N_total rows, ng) <- row block of N rows at n-tile offset `off` (or interleaved)
+  const int ncu = e->num_cu;
+  auto retiled = [&](const tts_tensor_desc& d, bf16_t* dst, int N, int K, int N_total, int ng,
+                     int mult, int off) {
     upload_bf16(d, staging.as<bf16_t>(), s, staging32);
-    launch_retile(staging.as<bf16_t>(), dst, N, K, s, mult, off);
+    launch_retile(staging.as<bf16_t>(), dst, N, K, N_total, ng, ncu, s, mult, off);
     HIP_CHECK(hipGetLastError());
   };
-  const int KT_h = HID / 32;
   for (int l = 0; l < L; ++l) {
     LmLayer& ly = M.layers[l];
     const std::string pre = "model.layers." + std::to_string(l) + ".";
     upload_bf16(tm.get(pre + "input_layernorm.weight", {HID}), ly.ln1, s, staging32);
     upload_bf16(tm.get(pre + "post_attention_layernorm.weight", {HID}), ly.ln2, s, staging32);
-    retiled(tm.get(pre + "self_attn.q_proj.weight", {H * D, HID}), ly.wqkv, H * D, HID, 1, 0);
-    retiled(tm.get(pre + "self_attn.k_proj.weight", {KVH * D, HID}),
-            ly.wqkv + (size_t)(H * D / 16) * KT_h * 512, KVH * D, HID, 1, 0);
-    retiled(tm.get(pre + "self_attn.v_proj.weight", {KVH * D, HID}),
-            ly.wqkv + (size_t)((H + KVH) * D / 16) * KT_h * 512, KVH * D, HID, 1, 0);
-    retiled(tm.get(pre + "self_attn.o_proj.weight", {HID, H * D}), ly.wo, HID, H * D, 1, 0);
-    retiled(tm.get(pre + "mlp.gate_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2, 0);
-    retiled(tm.get(pre + "mlp.up_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2, 1);
-    retiled(tm.get(pre + "mlp.down_proj.weight", {HID, FF}), ly.wd, HID, FF, 1, 0);
+    retiled(tm.get(pre + "self_attn.q_proj.weight", {H * D, HID}), ly.wqkv, H * D, HID, QKV, 1, 1, 0);
+    retiled(tm.get(pre + "self_attn.k_proj.weight", {KVH * D, HID}), ly.wqkv, KVH * D, HID, QKV, 1, 1,
+            H * D / 16);
+    retiled(tm.get(pre + "self_attn.v_proj.weight", {KVH * D, HID}), ly.wqkv, KVH * D, HID, QKV, 1, 1,
+            (H + KVH) * D / 16);
+    retiled(tm.get(pre + "self_attn.o_proj.weight", {HID, H * D}), ly.wo, HID, H * D, HID, 1, 1, 0);
+    retiled(tm.get(pre + "mlp.gate_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2 * FF, 2, 2, 0);
+    retiled(tm.get(pre + "mlp.up_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2 * FF, 2, 2, 1);
+    retiled(tm.get(pre + "mlp.down_proj.weight", {HID, FF}), ly.wd, HID, FF, HID, 1, 1, 0);
   }
   upload_bf16(tm.get("model.norm.weight", {HID}), M.final_norm, s, staging32);
   const tts_tensor_desc& emb = tm.get("model.embed_tokens.weight", {V, HID});
   M.embed_rows.alloc((size_t)V * HID * 2);
   upload_bf16(emb, M.embed_rows.as<bf16_t>(), s, staging32);
   if (c.tie_word_embeddings) {
-    launch_retile(M.embed_rows.as<bf16_t>(), M.lm_head, V, HID, s, 1, 0);
+    launch_retile(M.embed_rows.as<bf16_t>(), M.lm_head, V, HID, V, 1, ncu, s, 1, 0);
   } else {
-    retiled(tm.get("lm_head.weight", {V, HID}), M.lm_head, V, HID, 1, 0);
+    retiled(tm.get("lm_head.weight", {V, HID}), M.lm_head, V, HID, V, 1, 1, 0);
   }
 
   // ---- RoPE table
@@ -313,63 +315,36 @@ struct Ctx {
   }
 
   // One transformer stack pass over `rows` rows held in w.x.
-  // Decode-step cache warming: the latency-bound launches of a layer
-  // (qkv, attention, o_proj, down) leave CUs idle; extra workgroups on those CUs read the
-  // weights the following launches will stream, so that HBM time overlaps the latency
-  // chains and the consumers find the lines in the Infinity Cache.  The layer's matrices
-  // are contiguous in the slab (wqkv | wo | wgu | wd | next layer), so each warm-up is
-  // one byte range.
-  static Prefetch pf_range(const void* base, size_t off, size_t bytes, int wgs) {
-    Prefetch p;
-    p.ptr = (const char*)base + off;
-    p.bytes = bytes;
-    p.wgs = wgs;
-    return p;
-  }
-
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
-    const bool warm = decode && e->prefetch;
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
-      const size_t wo_b = (size_t)HID * HD * 2, wgu_b = (size_t)2 * FF * HID * 2;
-      const size_t wd_b = (size_t)HID * FF * 2;
-      const size_t gu_a = wgu_b * 3 / 5;  // share of wgu warmed during attention
-      WgemmArgs exq;
-      if (warm) exq.pf = pf_range(ly.wo, 0, wo_b, 64);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(),
-           nullptr, EPI_STORE, &exq);
+           nullptr, EPI_STORE);
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
       // decode with few rows: the o_proj prologue merges the attention chunks itself
       const bool fuse_combine = decode && rows <= kPrefillChunk &&
                                 plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
       if (decode) {
-        if (warm) a.pf = pf_range(ly.wgu, 0, gu_a, 192);
         launch_attn_decode_step(a, s);
       } else {
         launch_rope_append(a, s);
         launch_attn_decode(a, false, s);
       }
-      WgemmArgs exo;
-      if (warm) exo.pf = pf_range(ly.wgu, gu_a, wgu_b - gu_a + wd_b / 2, 128);
       if (fuse_combine) {
+        WgemmArgs exo;
         exo.attn_o = a.part_o; exo.attn_ml = a.part_ml; exo.attn_pos = pos;
         exo.attn_split = a.split; exo.attn_nsplit = a.nsplit; exo.attn_D = a.D;
         gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &exo);
       } else {
         launch_attn_combine(a, s);
         gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
-             w.x.as<bf16_t>(), EPI_RESID, &exo);
+             w.x.as<bf16_t>(), EPI_RESID);
       }
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
-      WgemmArgs exd;
-      if (warm && l + 1 < c.num_layers) {  // next layer's norms + qkv projection
-        const LmLayer& nx = M.layers[l + 1];
-        exd.pf = pf_range(nx.ln1, 0, (size_t)(nx.wo - nx.ln1) * 2, 128);
-      }
       gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),
-           EPI_RESID, &exd);
+           EPI_RESID);
     }
   }
 

@@ -20,17 +20,19 @@
 // A operand; at M = 1 fifteen of the sixteen A rows are zero, which costs nothing because
 // the kernel is HBM-bound on the weight stream.
 #include <algorithm>
+#include <cstdio>
+#include <stdexcept>
 
-#include "hip_common.h"
-#include "lm_kernels.h"
+#include "lm_gemm_kernel.h"
 
 namespace tts {
 
 // ---------------------------------------------------------------- weight re-layout ----
 __global__ void retile_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ t, int N,
-                              int K, int nt_mult, int nt_off) {
+                              int K, int nt_mult, int nt_off, StreamPlan p, int units) {
   const int KT = K / 32;
   const long long nchunks = (long long)(N / 16) * KT * 64;
+  const int ur = p.ur();
   for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < nchunks;
        c += (long long)gridDim.x * blockDim.x) {
     const int lane = (int)(c & 63);
@@ -40,587 +42,80 @@ __global__ void retile_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__
     const int n = nt * 16 + (lane & 15);
     const int k = kt * 32 + 8 * (lane >> 4);
     const u32x4_t v = *(const u32x4_t*)(w + (size_t)n * K + k);
-    const long long dtile = (long long)(nt * nt_mult + nt_off) * KT + kt;
+    const long long dtile = plan_tile(p.ng, p.ksplit, p.ku, ur, units, KT, nt * nt_mult + nt_off, kt);
     *(u32x4_t*)(t + (size_t)(dtile * 64 + lane) * 8) = v;
   }
 }
 
-void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, hipStream_t s, int nt_mult,
-                   int nt_off) {
+void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, int N_total, int ng, int num_cu,
+                   hipStream_t s, int nt_mult, int nt_off) {
+  const StreamPlan p = stream_plan(N_total, K, ng, num_cu);
+  const int units = (N_total / 16) / ng;
   long long nchunks = (long long)(N / 16) * (K / 32) * 64;
   int grid = (int)((nchunks + 255) / 256);
   if (grid > 65536) grid = 65536;
-  hipLaunchKernelGGL(retile_kernel, dim3(grid), dim3(256), 0, s, w, t, N, K, nt_mult, nt_off);
+  hipLaunchKernelGGL(retile_kernel, dim3(grid), dim3(256), 0, s, w, t, N, K, nt_mult, nt_off, p, units);
 }
 
-// ---------------------------------------------------------------- the GEMM kernel -----
-// One workgroup = WAVES waves; KSPLIT consecutive waves split the K range of one unit
-// (a unit = NG n-tiles of 16 output columns), WAVES/KSPLIT units run side by side, and
-// the workgroup walks units grid-stride.  Each wave streams its weight tiles in stages
-// of KU tiles (KU KiB), double-buffered, and the stream never stops: the first stage is
-// issued before the A-operand prologue (RMSNorm / attention combine), and the last stage
-// of a unit prefetches the first stage of the wave's next unit.
-TTS_DEV bf16x8_t as_bf16x8(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v); }
-
-// Better (value, index): larger value wins, lower index on ties (torch.argmax semantics).
-TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
-  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+static bool shape_fits(int c, int KT, int ng) {
+  const Shape3& h = kShapes[c];
+  return shape_ng2(c) == (ng == 2) && KT % (h.ksplit * h.ku) == 0 && h.waves % h.ksplit == 0;
 }
 
-constexpr int A_GLOBAL = 0, A_LDS = 1, A_ATTN = 2;
-
-// MT_MAX: compile-time bound on 16-row m-tiles (1 for decode, 4 for up to 64 rows)
-template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI>
-__global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NT = WAVES * 64;
-  constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
-  if ((int)blockIdx.x >= a.real_grid) {
-    prefetch_role(a.pf.ptr, a.pf.bytes, blockIdx.x - a.real_grid, gridDim.x - a.real_grid);
-    return;
+// The stream plan of a matrix (its tile layout and its decode launch).  Chosen from the
+// HBM streaming sweeps (scripts/hbm_floor.hip, scripts/wgemm_probe.cpp): one workgroup per
+// CU where the units allow it, many waves each with a few KiB in flight, stage-interleaved.
+StreamPlan stream_plan(int N, int K, int ng, int num_cu) {
+  const int units = (N / 16) / ng;
+  const int KT = K / 32;
+  int c;
+  if (ng == 2) c = 5;
+  else if (units >= 4 * num_cu) c = 0;
+  else if (K >= 4096) c = 3;
+  else c = 2;
+  // experiment hook (scripts/wgemm_probe.cpp): TTS_STREAM_PLAN=<shape index>[,grid]
+  static const char* forced = getenv("TTS_STREAM_PLAN");
+  int fgrid = 0;
+  if (forced) {
+    int fc = -1;
+    sscanf(forced, "%d,%d", &fc, &fgrid);
+    if (fc >= 0 && fc < kNumShapes && shape_fits(fc, KT, ng)) c = fc;
   }
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int kpart = wave % KSPLIT;
-  const int ugrp = wave / KSPLIT;
-  const int M = a.M;
-  const int mtn = (M + 15) >> 4;
-  const int KT = a.K >> 5;
-  const int units = (a.N >> 4) / NG;
-  const int kt_per = KT / KSPLIT;
-  const int kt0 = kpart * kt_per;
-  const int kend = kt0 + kt_per;
-  const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
-  const int ustride = a.real_grid * UPW;
-
-  bf16_t* xs = (bf16_t*)smem;
-  const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
-  float* red = (float*)(smem + xs_bytes);  // [WAVES][NG*MT_MAX*4][64] split-K partials
-  float* xtra = red + WAVES * NG * MT_MAX * 4 * 64 + 64;  // A_ATTN scratch
-
-  // ---- operands of the prologue and epilogue are loaded FIRST, the weight stream after:
-  // vmcnt retires in issue order, so anything issued behind the stream could not be used
-  // before the whole first weight stage had landed.
-  const int tid = threadIdx.x;
-  const int kch = a.K >> 3;  // 16-B chunks per A row
-  // (a) A rows (+ RMSNorm weight) for the LDS prologue, EA chunks per thread at most
-  constexpr int EA = 4;
-  const int achunks = M * kch;
-  const int a_nj = (achunks + NT - 1) / NT;
-  const bool early_a = (ASRC == A_LDS) && a_nj <= EA && (kch & 63) == 0;
-  u32x4_t xe[EA], ne[EA];
-  if constexpr (ASRC == A_LDS) {
-    if (early_a) {
-#pragma unroll
-      for (int j = 0; j < EA; ++j) {
-        if (j < a_nj) {  // uniform
-          const int c = min(tid + j * NT, achunks - 1);
-          const int m = c / kch, k = (c - m * kch) * 8;
-          xe[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
-          if constexpr (NORM) ne[j] = *(const u32x4_t*)(a.normw + k);
-        }
-      }
-    }
+  if (!shape_fits(c, KT, ng)) {  // small test shapes
+    c = -1;
+    for (int t = 0; t < kNumShapes && c < 0; ++t)
+      if (shape_fits(t, KT, ng)) c = t;
+    if (c < 0) throw std::runtime_error("no stream plan fits K");
   }
-  // (b) attention chunk partials for the o_proj prologue: thread = (row, 8 dims) item x
-  //     chunk group; every chunk statistic of the item's head, CPG chunk vectors
-  constexpr int NSX = 8, CPG = (WAVES >= 16) ? 2 : 4;
-  const int NS = a.attn_nsplit;
-  const int aitems = M * kch;
-  const int agroups = (ASRC == A_ATTN && aitems <= NT) ? NT / aitems : 0;
-  const int acpg = agroups ? (NS + agroups - 1) / agroups : CPG + 1;
-  const bool early_o = (ASRC == A_ATTN) && agroups > 0 && NS <= NSX && acpg <= CPG;
-  float2 mle[NSX], mlo[CPG];
-  float4 poe[CPG][2];
-  int pose = 0;
-  if constexpr (ASRC == A_ATTN) {
-    if (early_o) {
-      const int it = tid % aitems, grp = min(tid / aitems, agroups - 1);
-      const int D = a.attn_D, H = a.K / D;
-      const int m = it / kch, hd = (it - m * kch) * 8;
-      const size_t mh = (size_t)m * H + hd / D;
-      const int d = hd % D;
-      pose = a.attn_pos[m];
-#pragma unroll
-      for (int s = 0; s < NSX; ++s) mle[s] = *(const float2*)(a.attn_ml + (mh * NS + min(s, NS - 1)) * 2);
-#pragma unroll
-      for (int i = 0; i < CPG; ++i) {
-        const int s = min(grp * acpg + i, NS - 1);
-        const float* po = a.attn_o + (mh * NS + s) * D + d;
-        poe[i][0] = *(const float4*)po;
-        poe[i][1] = *(const float4*)(po + 4);
-        mlo[i] = *(const float2*)(a.attn_ml + (mh * NS + s) * 2);
-      }
-    }
-  }
-  // (c) epilogue operands of the wave's first unit: residual values / EOS mask + seen bits
-  int u = blockIdx.x * UPW + ugrp;
-  const int u_first = min(u, units - 1);
-  bf16_t rre[MT_MAX][4];
-  int eosr[MT_MAX][4];
-  uint32_t seen_cur[MT_MAX][4];
-#pragma unroll
-  for (int mt = 0; mt < MT_MAX; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (mt < mtn) {
-        const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
-        if constexpr (EPI == EPI_RESID) rre[mt][r] = a.resid[(size_t)m * a.ldo + u_first * 16 + (lane & 15)];
-        if constexpr (EPI == EPI_LOGITS) {
-          eosr[mt][r] = a.eos_mask[m];
-          seen_cur[mt][r] = a.seen[(size_t)m * a.seen_stride + (u_first >> 1)];
-        }
-      }
-    }
-
-  // ---- then the weight stream
-  u32x4_t wb[KU][NG];
-  auto wptr = [&](int uu, int g) {
-    return (const u32x4_t*)(a.w + ((size_t)(uu * NG + g) * KT) * 512) + lane;
-  };
-  if (u < units) {
-#pragma unroll
-    for (int kk = 0; kk < KU; ++kk)
-#pragma unroll
-      for (int g = 0; g < NG; ++g) wb[kk][g] = __builtin_nontemporal_load(wptr(u, g) + (kt0 + kk) * 64);
-  }
-
-  // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
-  if constexpr (ASRC == A_LDS) {
-   if (early_a) {
-    // rows already in registers: RMSNorm statistics per 64-chunk wave segment (DPP), the
-    // segments of a row summed in fixed order after one barrier
-    if constexpr (NORM) {
-#pragma unroll
-      for (int j = 0; j < EA; ++j) {
-        if (j < a_nj) {
-          float s = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = bf_lo(xe[j][q]), hi = bf_hi(xe[j][q]);
-            s += lo * lo + hi * hi;
-          }
-          s = wave_sum_dpp(s);
-          const int c = tid + j * NT;
-          if (lane == 0 && c < achunks) red[c >> 6] = s;
-        }
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < EA; ++j) {
-      if (j < a_nj) {
-        const int c = tid + j * NT;
-        if (c < achunks) {
-          const int m = c / kch, k = (c - m * kch) * 8;
-          u32x4_t v = xe[j];
-          if constexpr (NORM) {
-            const int seg0 = (m * kch) >> 6, nseg = kch >> 6;
-            float ss = 0.f;
-            for (int sg = 0; sg < nseg; ++sg) ss += red[seg0 + sg];
-            const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float lo = rbf(bf_lo(ne[j][q]) * rbf(bf_lo(v[q]) * r));
-              const float hi = rbf(bf_hi(ne[j][q]) * rbf(bf_hi(v[q]) * r));
-              v[q] = pack_bf2(lo, hi);
-            }
-          }
-          *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v;
-        }
-      }
-    }
-    __syncthreads();
-   } else {
-    // rows in parallel: wave w stages rows w, w+WAVES, ... (DPP row reduction, no barrier)
-    // One pass per row, all of a lane's 16-B chunks in flight at once (K <= 4096 for the
-    // RMSNorm'ed rows; longer plain rows go in batches of 8 chunks).
-    constexpr int CPL = 8;  // chunks per lane held in registers
-    for (int m = wave; m < M; m += WAVES) {
-      const bf16_t* xr = a.x + (size_t)m * a.ldx;
-      for (int k0 = 0; k0 < a.K; k0 += 64 * 8 * CPL) {
-        u32x4_t xv[CPL];
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const int k = k0 + (c * 64 + lane) * 8;
-          if (k < a.K) xv[c] = *(const u32x4_t*)(xr + k);
-        }
-        if constexpr (NORM) {  // (K <= 64*8*CPL: the whole row is in xv)
-          float ss = 0.f;
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            if ((c * 64 + lane) * 8 < a.K) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const float lo = bf_lo(xv[c][q]), hi = bf_hi(xv[c][q]);
-                ss += lo * lo + hi * hi;
-              }
-            }
-          }
-          ss = wave_sum_dpp(ss);
-          const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            const int k = (c * 64 + lane) * 8;
-            if (k < a.K) {
-              const u32x4_t g = *(const u32x4_t*)(a.normw + k);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const float lo = rbf(bf_lo(g[q]) * rbf(bf_lo(xv[c][q]) * r));
-                const float hi = rbf(bf_hi(g[q]) * rbf(bf_hi(xv[c][q]) * r));
-                xv[c][q] = pack_bf2(lo, hi);
-              }
-            }
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const int k = k0 + (c * 64 + lane) * 8;
-          if (k < a.K) *(u32x4_t*)(xs + (size_t)m * ldxs + k) = xv[c];
-        }
-      }
-    }
-    __syncthreads();
-   }
-  } else if constexpr (ASRC == A_ATTN) {
-   if (early_o) {
-    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
-    const int it = tid % aitems, grp = tid / aitems;
-    const int ns = (pose + a.attn_split) / a.attn_split;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int s = 0; s < NSX; ++s) if (s < ns) mx = fmaxf(mx, mle[s].x);
-    float l = 0.f;
-#pragma unroll
-    for (int s = 0; s < NSX; ++s) if (s < ns) l += mle[s].y * expf(mle[s].x - mx);
-    const float il = 1.0f / l;
-    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < CPG; ++i) {
-      const int s = grp * acpg + i;
-      if (i < acpg && s < ns) {
-        const float fs = expf(mlo[i].x - mx) * il;
-        o[0] += poe[i][0].x * fs; o[1] += poe[i][0].y * fs; o[2] += poe[i][0].z * fs; o[3] += poe[i][0].w * fs;
-        o[4] += poe[i][1].x * fs; o[5] += poe[i][1].y * fs; o[6] += poe[i][1].z * fs; o[7] += poe[i][1].w * fs;
-      }
-    }
-    const int m = it / kch, hd = (it - m * kch) * 8;
-    if (agroups > 1) {  // chunk groups of an item summed in fixed order through LDS
-      if (grp < agroups) {
-        float4* op = (float4*)xtra + (size_t)(grp * aitems + it) * 2;
-        op[0] = make_float4(o[0], o[1], o[2], o[3]);
-        op[1] = make_float4(o[4], o[5], o[6], o[7]);
-      }
-      __syncthreads();
-      if (grp == 0) {
-        for (int g = 1; g < agroups; ++g) {
-          const float4* op = (const float4*)xtra + (size_t)(g * aitems + it) * 2;
-          const float4 v0 = op[0], v1 = op[1];
-          o[0] += v0.x; o[1] += v0.y; o[2] += v0.z; o[3] += v0.w;
-          o[4] += v1.x; o[5] += v1.y; o[6] += v1.z; o[7] += v1.w;
-        }
-      }
-    }
-    if (grp == 0) {
-      u32x4_t pk;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
-      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
-    }
-    __syncthreads();
-   } else {
-    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
-    // phase 1: one thread per (row, head) turns the chunk statistics into factors (LDS);
-    // phase 2: every thread merges its (row, head, dim) elements with independent loads.
-    const int D = a.attn_D, H = a.K / D, NS = a.attn_nsplit;
-    float* fac = xtra;
-    for (int mh = threadIdx.x; mh < M * H; mh += NT) {
-      const int m = mh / H;
-      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
-      const float* ml = a.attn_ml + (size_t)mh * NS * 2;
-      float mx = -INFINITY;
-      for (int s = 0; s < ns; ++s) mx = fmaxf(mx, ml[2 * s]);
-      float l = 0.f;
-      for (int s = 0; s < ns; ++s) {
-        const float f = expf(ml[2 * s] - mx);
-        fac[mh * NS + s] = f;
-        l += ml[2 * s + 1] * f;
-      }
-      const float il = 1.0f / l;
-      for (int s = 0; s < ns; ++s) fac[mh * NS + s] *= il;
-    }
-    __syncthreads();
-    // 8 consecutive dims per thread: two float4 loads per chunk, one 16-B LDS store
-    for (int e = threadIdx.x; e < M * a.K / 8; e += NT) {
-      const int m = (e * 8) / a.K, hd = (e * 8) % a.K, mh = m * H + hd / D, d = hd % D;
-      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
-      const float* po = a.attn_o + (size_t)mh * NS * D + d;
-      const float* f = fac + mh * NS;
-      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int s = 0; s < ns; ++s) {
-        const float4 v0 = *(const float4*)(po + (size_t)s * D);
-        const float4 v1 = *(const float4*)(po + (size_t)s * D + 4);
-        const float fs = f[s];
-        o[0] += v0.x * fs; o[1] += v0.y * fs; o[2] += v0.z * fs; o[3] += v0.w * fs;
-        o[4] += v1.x * fs; o[5] += v1.y * fs; o[6] += v1.z * fs; o[7] += v1.w * fs;
-      }
-      u32x4_t pk;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
-      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
-    }
-    __syncthreads();
-   }
-  }
-
-  const int arow = lane & 15;
-  const int akoff = 8 * (lane >> 4);
-
-  // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
-  float best_v[MT_MAX][4];
-  int best_i[MT_MAX][4];
-#pragma unroll
-  for (int mt = 0; mt < MT_MAX; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { best_v[mt][r] = -INFINITY; best_i[mt][r] = 0x7fffffff; }
-
-  bool first = true;
-  for (int ubase = blockIdx.x * UPW; ubase < units; ubase += ustride) {
-    u = ubase + ugrp;
-    const bool active = u < units;
-    uint32_t seen_nxt[MT_MAX][4];
-    if constexpr (EPI == EPI_LOGITS) {  // next unit's penalty bits, in flight with this unit
-      const int un = min(u + ustride, units - 1);
-#pragma unroll
-      for (int mt = 0; mt < MT_MAX; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (mt < mtn) {
-            const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
-            seen_nxt[mt][r] = a.seen[(size_t)m * a.seen_stride + (un >> 1)];
-          }
-    }
-    f32x4_t acc[NG][MT_MAX];
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    if (active) {
-      const int unext = u + ustride;
-      for (int kt = kt0; kt < kend; kt += KU) {
-        // next stage: same unit, else the first stage of the wave's next unit
-        int nu = u, nk = kt + KU;
-        if (nk >= kend) { nu = unext; nk = kt0; }
-        const bool has_next = nu < units;
-        u32x4_t wn[KU][NG];
-        if (has_next) {
-#pragma unroll
-          for (int kk = 0; kk < KU; ++kk)
-#pragma unroll
-            for (int g = 0; g < NG; ++g) wn[kk][g] = __builtin_nontemporal_load(wptr(nu, g) + (nk + kk) * 64);
-        }
-
-#pragma unroll
-        for (int kk = 0; kk < KU; ++kk) {
-          const int k = (kt + kk) * 32 + akoff;
-#pragma unroll
-          for (int mt = 0; mt < MT_MAX; ++mt) {
-            if (mt < mtn) {
-              const int m = mt * 16 + arow;
-              u32x4_t av = u32x4_t{0u, 0u, 0u, 0u};
-              if (m < M) {
-                if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
-                else av = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
-              }
-              const bf16x8_t af = as_bf16x8(av);
-#pragma unroll
-              for (int g = 0; g < NG; ++g)
-                acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, as_bf16x8(wb[kk][g]),
-                                                                     acc[g][mt], 0, 0, 0);
-            }
-          }
-        }
-        if (has_next) {
-#pragma unroll
-          for (int kk = 0; kk < KU; ++kk)
-#pragma unroll
-            for (int g = 0; g < NG; ++g) wb[kk][g] = wn[kk][g];
-        }
-      }
-    }
-
-    // ---- split-K combine through LDS, fixed order (deterministic)
-    if constexpr (KSPLIT > 1) {
-      constexpr int PS = NG * MT_MAX * 4 * 64;
-      float* myred = red + (size_t)wave * PS;
-#pragma unroll
-      for (int g = 0; g < NG; ++g)
-#pragma unroll
-        for (int mt = 0; mt < MT_MAX; ++mt)
-          if (mt < mtn) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
-          }
-      __syncthreads();
-      if (kpart == 0) {
-#pragma unroll
-        for (int p = 1; p < KSPLIT; ++p) {
-          const float* o = red + (size_t)(wave + p) * PS;
-#pragma unroll
-          for (int g = 0; g < NG; ++g)
-#pragma unroll
-            for (int mt = 0; mt < MT_MAX; ++mt)
-              if (mt < mtn) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[g][mt][r] += o[((g * MT_MAX + mt) * 4 + r) * 64 + lane];
-              }
-        }
-      }
-      __syncthreads();
-    }
-
-    // ---- epilogue (lane owns column n, rows m = mt*16 + 4*(lane>>4) + r)
-    if (kpart == 0 && active) {
-      const int n = u * 16 + (lane & 15);
-#pragma unroll
-      for (int mt = 0; mt < MT_MAX; ++mt) {
-        if (mt >= mtn) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = mt * 16 + 4 * (lane >> 4) + r;
-          if (m >= M) continue;
-          if constexpr (EPI == EPI_STORE) {
-            a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
-          } else if constexpr (EPI == EPI_RESID) {
-            bf16_t* p = a.resid + (size_t)m * a.ldo + n;
-            *p = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
-          } else if constexpr (EPI == EPI_SWIGLU) {
-            // unit u = (gate tile, up tile) pair for intermediate columns u*16 .. u*16+15
-            const float gt = rbf(acc[0][mt][r]);
-            const float up = rbf(acc[NG - 1][mt][r]);
-            a.out[(size_t)m * a.ldo + n] = f2bf(rbf(silu_f(gt)) * up);
-          } else if constexpr (EPI == EPI_LOGITS) {
-            float v = rbf(acc[0][mt][r]);  // logits are materialised in bf16, then .float()
-            const uint32_t bits = seen_cur[mt][r];
-            if ((bits >> (n & 31)) & 1u) v = (v < 0.f) ? v * a.penalty : v / a.penalty;
-            if (n == eosr[mt][r]) v = -INFINITY;
-            argmax_merge(best_v[mt][r], best_i[mt][r], v, n);
-          }
-        }
-      }
-    }
-    first = false;
-    if constexpr (EPI == EPI_LOGITS) {
-#pragma unroll
-      for (int mt = 0; mt < MT_MAX; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) seen_cur[mt][r] = seen_nxt[mt][r];
-    }
-  }
-
-  if constexpr (EPI == EPI_LOGITS) {
-    // lanes sharing (lane >> 4) hold the same rows: butterfly over the 16 columns
-#pragma unroll
-    for (int mt = 0; mt < MT_MAX; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          const float v2 = __shfl_xor(best_v[mt][r], o, 64);
-          const int i2 = __shfl_xor(best_i[mt][r], o, 64);
-          argmax_merge(best_v[mt][r], best_i[mt][r], v2, i2);
-        }
-    // across the unit-groups of the workgroup (only kpart==0 waves hold results)
-    float* rv = red;
-    int* ri = (int*)(red + UPW * MT_MAX * 16);
-    __syncthreads();
-    if (kpart == 0 && (lane & 15) == 0) {
-#pragma unroll
-      for (int mt = 0; mt < MT_MAX; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = mt * 16 + 4 * (lane >> 4) + r;
-          rv[ugrp * MT_MAX * 16 + m] = best_v[mt][r];
-          ri[ugrp * MT_MAX * 16 + m] = best_i[mt][r];
-        }
-    }
-    __syncthreads();
-    for (int m = threadIdx.x; m < M; m += NT) {
-      float v = rv[m];
-      int i = ri[m];
-      for (int g = 1; g < UPW; ++g) argmax_merge(v, i, rv[g * MT_MAX * 16 + m], ri[g * MT_MAX * 16 + m]);
-      a.part_val[(size_t)m * a.part_stride + blockIdx.x] = v;
-      a.part_idx[(size_t)m * a.part_stride + blockIdx.x] = i;
-    }
-  }
+  StreamPlan p;
+  p.ng = ng;
+  p.waves = kShapes[c].waves;
+  p.ku = kShapes[c].ku;
+  p.ksplit = kShapes[c].ksplit;
+  const int upw = p.waves / p.ksplit;
+  int grid = (units + upw - 1) / upw;
+  // one workgroup per CU (lm_head: rounds of 4 units per workgroup); the argmax partials of
+  // EPI_LOGITS hold at most LOGITS_MAX_PARTS workgroups
+  const int cap = (fgrid > 0) ? std::min(fgrid, LOGITS_MAX_PARTS) : num_cu;
+  p.grid = std::min(grid, cap);
+  return p;
 }
 
-// ---------------------------------------------------------------- host dispatch -------
-// Launch shapes (WAVES, KU, KSPLIT): a small fixed table keeps the instantiation count low.
-enum { CFG_WIDE = 0, CFG_K2 = 1, CFG_K8 = 3, CFG_K4 = 4, CFG_K4W8 = 5, CFG_K16 = 6 };
-
-template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI>
-static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
-  const int mt = a.M <= 16 ? 1 : 4;
-  size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
-  lds += (size_t)(WAVES * NG * mt * 4 * 64 + 64) * sizeof(float);
-  if (ASRC == A_ATTN)  // chunk factors (fallback path) or chunk-group partials (early path)
-    lds += std::max((size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit, (size_t)WAVES * 64 * 8) * sizeof(float);
-  if (mt == 1) {
-    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
-                       dim3(WAVES * 64), lds, s, a);
-  } else if constexpr (WAVES <= 8) {  // 16-wave shapes are planned for M <= 16 only
-    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 4, NG, KSPLIT, ASRC, NORM, EPI>), dim3(grid),
-                       dim3(WAVES * 64), lds, s, a);
-  }
+static int shape_index(const StreamPlan& p) {
+  for (int c = 0; c < kNumShapes; ++c)
+    if (kShapes[c].waves == p.waves && kShapes[c].ku == p.ku && kShapes[c].ksplit == p.ksplit &&
+        shape_ng2(c) == (p.ng == 2))
+      return c;
+  return -1;
 }
 
-template <int NG, int ASRC, bool NORM, int EPI>
-static void launch_cfg(const WgemmArgs& a, int cfg, int grid, hipStream_t s) {
-  switch (cfg) {
-    case CFG_WIDE: launch_one<4, 8, NG, 1, ASRC, NORM, EPI>(a, grid, s); break;
-    case CFG_K2: launch_one<4, 8, NG, 2, ASRC, NORM, EPI>(a, grid, s); break;
-    case CFG_K8: launch_one<8, 8, NG, 8, ASRC, NORM, EPI>(a, grid, s); break;
-    case CFG_K4W8: launch_one<8, 8, NG, 4, ASRC, NORM, EPI>(a, grid, s); break;
-    case CFG_K16: launch_one<16, 8, NG, 16, ASRC, NORM, EPI>(a, grid, s); break;
-    default: launch_one<4, 8, NG, 4, ASRC, NORM, EPI>(a, grid, s); break;
-  }
-}
-
-// Chooses the launch shape so that every CU has work and enough bytes in flight: large-N
-// GEMMs (lm_head, MLP) stream whole n-tiles per wave; small-N projections split K across
-// the waves of a workgroup (and use 8-wave workgroups when only ~128 units exist).
 WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   WgemmPlan p;
-  const int NG = (epi == EPI_SWIGLU) ? 2 : 1;
-  const int units = (N / 16) / NG;
-  const int KT = K / 32;
+  const int ng = (epi == EPI_SWIGLU) ? 2 : 1;
+  p.sp = stream_plan(N, K, ng, num_cu);
+  p.cfg = shape_index(p.sp);
+  p.grid = p.sp.grid;
   p.a_lds = ((size_t)M * (K + 8) * 2) <= 80 * 1024;
-  int cfg, upw;
-  if (units >= num_cu * 4) { cfg = CFG_WIDE; upw = 4; }
-  else if (units >= num_cu * 2 && KT % 32 == 0) { cfg = CFG_K4W8; upw = 2; }
-  else if (units >= num_cu * 2 && KT % 16 == 0) { cfg = CFG_K2; upw = 2; }
-  else if (2 * units <= num_cu && KT % 128 == 0 && M <= 16) { cfg = CFG_K16; upw = 1; }
-  else if (KT % 64 == 0) { cfg = CFG_K8; upw = 1; }
-  else if (KT % 32 == 0) { cfg = CFG_K4; upw = 1; }
-  else { cfg = CFG_WIDE; upw = 4; }
-  // experiment hook (scripts/microbench.py): force a launch shape when it divides the shape
-  static const int forced = getenv("TTS_WGEMM_CFG") ? atoi(getenv("TTS_WGEMM_CFG")) : -1;
-  if (forced >= 0) {
-    const int ks[] = {1, 2, 0, 8, 4, 4, 16};
-    const int up[] = {4, 2, 0, 1, 1, 2, 1};
-    if (forced <= 6 && ks[forced] && KT % (ks[forced] * 8) == 0 && (forced != CFG_K16 || M <= 16)) {
-      cfg = forced;
-      upw = up[forced];
-    }
-  }
-  p.cfg = cfg;
-  int grid = (units + upw - 1) / upw;
-  const int cap = (epi == EPI_LOGITS) ? LOGITS_MAX_PARTS : num_cu * 8;
-  if (grid > cap) grid = cap;
-  p.grid = grid;
   return p;
 }
 
@@ -631,30 +126,14 @@ bool wgemm_supported(int M, int N, int K, int epi) {
 
 void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p, int epi, bool norm, hipStream_t s) {
   WgemmArgs a = a_in;
-  a.real_grid = p.grid;
-  const int grid = p.grid + ((a.pf.bytes && a.pf.ptr) ? a.pf.wgs : 0);
-  const int c = p.cfg;
-  const bool attn = a.attn_o != nullptr;
+  a.ur = p.sp.ur();
+  static const int diag = getenv("TTS_WGEMM_DIAG") ? atoi(getenv("TTS_WGEMM_DIAG")) : 0;
+  a.diag = diag;
   switch (epi) {
-    case EPI_STORE:
-      if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_STORE>(a, c, grid, s);
-      else if (norm) launch_cfg<1, A_LDS, true, EPI_STORE>(a, c, grid, s);
-      else launch_cfg<1, A_LDS, false, EPI_STORE>(a, c, grid, s);
-      break;
-    case EPI_RESID:
-      if (attn) launch_cfg<1, A_ATTN, false, EPI_RESID>(a, c, grid, s);
-      else if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_RESID>(a, c, grid, s);
-      else launch_cfg<1, A_LDS, false, EPI_RESID>(a, c, grid, s);
-      break;
-    case EPI_SWIGLU:
-      if (!p.a_lds) launch_cfg<2, A_GLOBAL, false, EPI_SWIGLU>(a, c, grid, s);
-      else if (norm) launch_cfg<2, A_LDS, true, EPI_SWIGLU>(a, c, grid, s);
-      else launch_cfg<2, A_LDS, false, EPI_SWIGLU>(a, c, grid, s);
-      break;
-    case EPI_LOGITS:  // the lm_head always carries the final RMSNorm (fused, or applied before)
-      if (!p.a_lds || !norm) launch_cfg<1, A_GLOBAL, false, EPI_LOGITS>(a, c, grid, s);
-      else launch_cfg<1, A_LDS, true, EPI_LOGITS>(a, c, grid, s);
-      break;
+    case EPI_STORE: launch_wgemm_store(a, p, norm, s); break;
+    case EPI_RESID: launch_wgemm_resid(a, p, norm, s); break;
+    case EPI_SWIGLU: launch_wgemm_swiglu(a, p, norm, s); break;
+    case EPI_LOGITS: launch_wgemm_logits(a, p, norm, s); break;
   }
 }
 

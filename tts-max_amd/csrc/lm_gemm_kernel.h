@@ -1,0 +1,615 @@
+// lm_gemm_kernel.h — the weight-streaming GEMM kernel template and its launch shapes,
+// instantiated per epilogue in lm_gemm_{store,resid,swiglu,logits}.hip (parallel builds).
+// See lm_gemm.hip for the design notes, the weight layout and the stream plans.
+#pragma once
+#include <algorithm>
+#include <cstdio>
+#include <stdexcept>
+
+#include "hip_common.h"
+#include "lm_kernels.h"
+
+namespace tts {
+
+// register budget of the early prologue: A chunks per thread / attention chunks per group
+constexpr int wgemm_ea(int waves) { return waves >= 16 ? 1 : (waves >= 8 ? 2 : 4); }
+constexpr int wgemm_cpg(int waves) { return waves >= 16 ? 2 : 4; }
+#define WGEMM_NSX 8
+inline bool wgemm_attn_early(int M, int K, int nsplit, int waves) {
+  const int aitems = M * (K / 8), NT = waves * 64;
+  if (aitems > NT || nsplit > WGEMM_NSX) return false;
+  const int groups = NT / aitems;
+  return (nsplit + groups - 1) / groups <= wgemm_cpg(waves);
+}
+
+// ---------------------------------------------------------------- the GEMM kernel -----
+// One workgroup = WAVES waves; KSPLIT consecutive waves split the K range of one unit
+// (a unit = NG n-tiles of 16 output columns), WAVES/KSPLIT units run side by side, and
+// the workgroup walks units grid-stride.  Each wave streams its weight tiles in stages
+// of KU tiles (KU KiB), double-buffered, and the stream never stops: the first stage is
+// issued before the A-operand prologue (RMSNorm / attention combine), and the last stage
+// of a unit prefetches the first stage of the wave's next unit.
+TTS_DEV bf16x8_t as_bf16x8(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+// Better (value, index): larger value wins, lower index on ties (torch.argmax semantics).
+TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+
+constexpr int A_GLOBAL = 0, A_LDS = 1, A_ATTN = 2;
+
+// MT_MAX: compile-time bound on 16-row m-tiles (1 for decode, 4 for up to 64 rows)
+template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R,
+          bool EARLY>
+__global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NT = WAVES * 64;
+  constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kpart = wave % KSPLIT;
+  const int ugrp = wave / KSPLIT;
+  const int M = a.M;
+  const int mtn = (M + 15) >> 4;
+  const int KT = a.K >> 5;
+  const int units = (a.N >> 4) / NG;
+  const int kt_per = KT / KSPLIT;
+  const int kt0 = kpart * kt_per;
+  const int kend = kt0 + kt_per;
+  const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
+  const int ustride = gridDim.x * UPW;
+
+  bf16_t* xs = (bf16_t*)smem;
+  const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
+  float* red = (float*)(smem + xs_bytes);  // [WAVES][NG*MT_MAX*4][64] split-K partials
+  float* xtra = red + WAVES * NG * MT_MAX * 4 * 64 + 64;  // A_ATTN scratch
+
+  // ---- operands of the prologue and epilogue are loaded FIRST, the weight stream after:
+  // vmcnt retires in issue order, so anything issued behind the stream could not be used
+  // before the whole first weight stage had landed.
+  const int tid = threadIdx.x;
+  const int kch = a.K >> 3;  // 16-B chunks per A row
+  // (a) A rows (+ RMSNorm weight) for the LDS prologue, EA chunks per thread at most
+  constexpr int EA = wgemm_ea(WAVES);
+  const int achunks = M * kch;
+  const int a_nj = (achunks + NT - 1) / NT;
+  constexpr bool early_a = EARLY && ASRC == A_LDS;  // (host: a_nj <= EA, kch % 64 == 0)
+  u32x4_t xe[EA], ne[EA];
+  if constexpr (early_a) {
+    {
+#pragma unroll
+      for (int j = 0; j < EA; ++j) {  // all EA issued (clamped): a fixed load count keeps the
+        const int c = min(tid + j * NT, achunks - 1);  // vmcnt waits below exact
+        const int m = c / kch, k = (c - m * kch) * 8;
+        xe[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+        if constexpr (NORM) ne[j] = *(const u32x4_t*)(a.normw + k);
+      }
+    }
+  }
+  // (b) attention chunk partials for the o_proj prologue: thread = (row, 8 dims) item x
+  //     chunk group; every chunk statistic of the item's head, CPG chunk vectors
+  constexpr int NSX = WGEMM_NSX, CPG = wgemm_cpg(WAVES);
+  const int NS = a.attn_nsplit;
+  const int aitems = M * kch;
+  const int agroups = (ASRC == A_ATTN && aitems <= NT) ? NT / aitems : 0;
+  const int acpg = agroups ? (NS + agroups - 1) / agroups : CPG + 1;
+  constexpr bool early_o = EARLY && ASRC == A_ATTN;  // (host: wgemm_attn_early)
+  float2 mle[NSX], mlo[CPG];
+  float4 poe[CPG][2];
+  int pose = 0;
+  if constexpr (early_o) {
+    {
+      const int it = tid % aitems, grp = min(tid / aitems, agroups - 1);
+      const int D = a.attn_D, H = a.K / D;
+      const int m = it / kch, hd = (it - m * kch) * 8;
+      const size_t mh = (size_t)m * H + hd / D;
+      const int d = hd % D;
+      pose = a.attn_pos[m];
+#pragma unroll
+      for (int s = 0; s < NSX; ++s) mle[s] = *(const float2*)(a.attn_ml + (mh * NS + min(s, NS - 1)) * 2);
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const int s = min(grp * acpg + i, NS - 1);
+        const float* po = a.attn_o + (mh * NS + s) * D + d;
+        poe[i][0] = *(const float4*)po;
+        poe[i][1] = *(const float4*)(po + 4);
+        mlo[i] = *(const float2*)(a.attn_ml + (mh * NS + s) * 2);
+      }
+    }
+  }
+  // (c) epilogue operands of the wave's first unit: residual values / EOS mask + seen bits
+  int u = blockIdx.x * UPW + ugrp;
+  const int u_first = min(u, units - 1);
+  bf16_t rre[MT_MAX][4];
+  int eosr[MT_MAX][4];
+  uint32_t seen_cur[MT_MAX][4];
+#pragma unroll
+  for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // (no mt < mtn test: loads behind a branch cost exact vmcnt)
+      const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
+      if constexpr (EPI == EPI_RESID) rre[mt][r] = a.resid[(size_t)m * a.ldo + u_first * 16 + (lane & 15)];
+      if constexpr (EPI == EPI_LOGITS) {
+        eosr[mt][r] = a.eos_mask[m];
+        seen_cur[mt][r] = a.seen[(size_t)m * a.seen_stride + (u_first >> 1)];
+      }
+    }
+
+  // ---- then the weight stream
+  // stage st of the wave's item of unit uu: NG*KU consecutive tiles (StreamPlan layout)
+  const int ur = a.ur;
+  auto sptr = [&](int uu, int st) {
+    uu = min(uu, units - 1);
+    const int r = uu / ur, ui = uu - r * ur;
+    const int nr = min(ur, units - r * ur);
+    const long long t = (long long)r * ur * KT * NG + (((long long)st * nr + ui) * KSPLIT + kpart) * NG * KU;
+    return (const u32x4_t*)a.w + t * 64 + lane;
+  };
+  // Register ring of R stages (S = stages per item, S % R == 0): the first R stages of the
+  // wave's stream are in flight before the prologue runs; consuming a slot refills it with
+  // the stage R positions later (next unit's stages once this unit's are all issued).
+  const int S = kt_per / KU;
+  u32x4_t wr[R][KU][NG];
+  int pu = u, ps = 0;  // next stage to issue
+  // The refills are issued only where the stage exists by construction (never behind a
+  // per-iteration condition): every path then has a fixed load count and the compiler's
+  // vmcnt waits stay exact (a conditional issue makes it merge paths pessimistically,
+  // i.e. drain the ring at every stage).
+  auto issue = [&](u32x4_t (&dst)[KU][NG]) {
+    const u32x4_t* q = sptr(pu, ps);
+#pragma unroll
+    for (int kk = 0; kk < KU; ++kk)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) dst[kk][g] = __builtin_nontemporal_load(q + (g * KU + kk) * 64);
+    if (++ps == S) { ps = 0; pu += ustride; }
+  };
+  // every wave's operand loads enter the CU's memory pipeline ahead of any weight load; the
+  // scheduling barrier stops the compiler sinking an operand load below the weight stream
+  // (each prologue wait would then drain the primed stages too)
+  __builtin_amdgcn_sched_barrier(0);
+  if (a.diag & 8) __syncthreads();
+  // (unconditional: a wave with no unit streams unit units-1, never consumed (sptr clamps).
+  // A branch here would make every prologue wait below drain the primed stages as well)
+#pragma unroll
+  for (int j = 0; j < R; ++j) issue(wr[j]);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
+  if (a.diag & 1) {
+  } else if constexpr (ASRC == A_LDS) {
+   if constexpr (early_a) {
+    // rows already in registers: RMSNorm statistics per 64-chunk wave segment (DPP), the
+    // segments of a row summed in fixed order after one barrier
+    if constexpr (NORM) {
+#pragma unroll
+      for (int j = 0; j < EA; ++j) {
+        if (j < a_nj) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = bf_lo(xe[j][q]), hi = bf_hi(xe[j][q]);
+            s += lo * lo + hi * hi;
+          }
+          s = wave_sum_dpp(s);
+          const int c = tid + j * NT;
+          if (lane == 0 && c < achunks) red[c >> 6] = s;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < EA; ++j) {
+      if (j < a_nj) {
+        const int c = tid + j * NT;
+        if (c < achunks) {
+          const int m = c / kch, k = (c - m * kch) * 8;
+          u32x4_t v = xe[j];
+          if constexpr (NORM) {
+            const int seg0 = (m * kch) >> 6, nseg = kch >> 6;
+            float ss = 0.f;
+            for (int sg = 0; sg < nseg; ++sg) ss += red[seg0 + sg];
+            const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float lo = rbf(bf_lo(ne[j][q]) * rbf(bf_lo(v[q]) * r));
+              const float hi = rbf(bf_hi(ne[j][q]) * rbf(bf_hi(v[q]) * r));
+              v[q] = pack_bf2(lo, hi);
+            }
+          }
+          *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v;
+        }
+      }
+    }
+    __syncthreads();
+   } else {
+    // general rows (more than the early registers hold): 16-B copies into LDS, 4 per
+    // thread in flight (clamped, unconditional loads), then RMSNorm in place, a wave per row
+    for (int c0 = 0; c0 < achunks; c0 += 4 * NT) {
+      u32x4_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = min(c0 + tid + j * NT, achunks - 1);
+        const int m = c / kch, k = (c - m * kch) * 8;
+        v[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + tid + j * NT;
+        if (c < achunks) {
+          const int m = c / kch, k = (c - m * kch) * 8;
+          *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v[j];
+        }
+      }
+    }
+    if constexpr (NORM) {
+      __syncthreads();
+      for (int m = wave; m < M; m += WAVES) {
+        bf16_t* xr = xs + (size_t)m * ldxs;
+        float ss = 0.f;
+        for (int k = lane * 8; k < a.K; k += 512) {
+          const u32x4_t v = *(const u32x4_t*)(xr + k);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = bf_lo(v[q]), hi = bf_hi(v[q]);
+            ss += lo * lo + hi * hi;
+          }
+        }
+        ss = wave_sum_dpp(ss);
+        const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+        for (int k = lane * 8; k < a.K; k += 512) {
+          u32x4_t v = *(const u32x4_t*)(xr + k);
+          const u32x4_t g = *(const u32x4_t*)(a.normw + k);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+          *(u32x4_t*)(xr + k) = v;
+        }
+      }
+    }
+    __syncthreads();
+   }
+  } else if constexpr (ASRC == A_ATTN) {
+   if constexpr (early_o) {
+    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
+    const int it = tid % aitems, grp = tid / aitems;
+    const int ns = (pose + a.attn_split) / a.attn_split;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < NSX; ++s) if (s < ns) mx = fmaxf(mx, mle[s].x);
+    float l = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSX; ++s) if (s < ns) l += mle[s].y * expf(mle[s].x - mx);
+    const float il = 1.0f / l;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < CPG; ++i) {
+      const int s = grp * acpg + i;
+      if (i < acpg && s < ns) {
+        const float fs = expf(mlo[i].x - mx) * il;
+        o[0] += poe[i][0].x * fs; o[1] += poe[i][0].y * fs; o[2] += poe[i][0].z * fs; o[3] += poe[i][0].w * fs;
+        o[4] += poe[i][1].x * fs; o[5] += poe[i][1].y * fs; o[6] += poe[i][1].z * fs; o[7] += poe[i][1].w * fs;
+      }
+    }
+    const int m = it / kch, hd = (it - m * kch) * 8;
+    if (agroups > 1) {  // chunk groups of an item summed in fixed order through LDS
+      if (grp < agroups) {
+        float4* op = (float4*)xtra + (size_t)(grp * aitems + it) * 2;
+        op[0] = make_float4(o[0], o[1], o[2], o[3]);
+        op[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
+      __syncthreads();
+      if (grp == 0) {
+        for (int g = 1; g < agroups; ++g) {
+          const float4* op = (const float4*)xtra + (size_t)(g * aitems + it) * 2;
+          const float4 v0 = op[0], v1 = op[1];
+          o[0] += v0.x; o[1] += v0.y; o[2] += v0.z; o[3] += v0.w;
+          o[4] += v1.x; o[5] += v1.y; o[6] += v1.z; o[7] += v1.w;
+        }
+      }
+    }
+    if (grp == 0) {
+      u32x4_t pk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
+      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
+    }
+    __syncthreads();
+   } else {
+    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
+    // phase 1: one thread per (row, head) turns the chunk statistics into factors (LDS);
+    // phase 2: every thread merges its (row, head, dim) elements with independent loads.
+    const int D = a.attn_D, H = a.K / D, NS = a.attn_nsplit;
+    float* fac = xtra;
+    for (int mh = threadIdx.x; mh < M * H; mh += NT) {
+      const int m = mh / H;
+      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
+      const float* ml = a.attn_ml + (size_t)mh * NS * 2;
+      float mx = -INFINITY;
+      for (int s = 0; s < ns; ++s) mx = fmaxf(mx, ml[2 * s]);
+      float l = 0.f;
+      for (int s = 0; s < ns; ++s) {
+        const float f = expf(ml[2 * s] - mx);
+        fac[mh * NS + s] = f;
+        l += ml[2 * s + 1] * f;
+      }
+      const float il = 1.0f / l;
+      for (int s = 0; s < ns; ++s) fac[mh * NS + s] *= il;
+    }
+    __syncthreads();
+    // 8 consecutive dims per thread: two float4 loads per chunk, one 16-B LDS store
+    for (int e = threadIdx.x; e < M * a.K / 8; e += NT) {
+      const int m = (e * 8) / a.K, hd = (e * 8) % a.K, mh = m * H + hd / D, d = hd % D;
+      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
+      const float* po = a.attn_o + (size_t)mh * NS * D + d;
+      const float* f = fac + mh * NS;
+      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int s = 0; s < ns; ++s) {
+        const float4 v0 = *(const float4*)(po + (size_t)s * D);
+        const float4 v1 = *(const float4*)(po + (size_t)s * D + 4);
+        const float fs = f[s];
+        o[0] += v0.x * fs; o[1] += v0.y * fs; o[2] += v0.z * fs; o[3] += v0.w * fs;
+        o[4] += v1.x * fs; o[5] += v1.y * fs; o[6] += v1.z * fs; o[7] += v1.w * fs;
+      }
+      u32x4_t pk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
+      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
+    }
+    __syncthreads();
+   }
+  }
+
+  const int arow = lane & 15;
+  const int akoff = 8 * (lane >> 4);
+
+  // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
+  float best_v[MT_MAX][4];
+  int best_i[MT_MAX][4];
+#pragma unroll
+  for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { best_v[mt][r] = -INFINITY; best_i[mt][r] = 0x7fffffff; }
+
+  bool first = true;
+  for (int ubase = blockIdx.x * UPW; ubase < units; ubase += ustride) {
+    u = ubase + ugrp;
+    const bool active = u < units;
+    uint32_t seen_nxt[MT_MAX][4];
+    if constexpr (EPI == EPI_LOGITS) {  // next unit's penalty bits, in flight with this unit
+      const int un = min(u + ustride, units - 1);
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
+          seen_nxt[mt][r] = a.seen[(size_t)m * a.seen_stride + (un >> 1)];
+        }
+    }
+    f32x4_t acc[NG][MT_MAX];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto consume = [&](const u32x4_t (&src)[KU][NG], int stage) {
+      const int kt = kt0 + stage * KU;
+#pragma unroll
+      for (int kk = 0; kk < KU; ++kk) {
+        const int k = (kt + kk) * 32 + akoff;
+#pragma unroll
+        for (int mt = 0; mt < MT_MAX; ++mt) {  // (all MT_MAX tiles: no branch, exact vmcnt)
+          const int m = min(mt * 16 + arow, M - 1);  // rows >= M: duplicates, never stored
+          u32x4_t av;
+          if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
+          else av = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+          const bf16x8_t af = as_bf16x8(av);
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+            acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, as_bf16x8(src[kk][g]),
+                                                                 acc[g][mt], 0, 0, 0);
+        }
+      }
+    };
+    if (u + ustride < units) {  // the wave has a next unit: every refill exists
+      for (int st = 0; st < S; st += R) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) { consume(wr[j], st + j); issue(wr[j]); }
+      }
+    } else {  // last unit of the wave (or none): refill while stages remain, then drain
+      for (int st = 0; st + R < S; st += R) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) { consume(wr[j], st + j); issue(wr[j]); }
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) consume(wr[j], S - R + j);
+    }
+
+    if (a.diag & 2) {
+      if (acc[0][0][0] == 1234.5f && a.out) a.out[0] = 0;
+      continue;
+    }
+    // ---- split-K combine through LDS, fixed order (deterministic)
+    if constexpr (KSPLIT > 1) {
+      constexpr int PS = NG * MT_MAX * 4 * 64;
+      float* myred = red + (size_t)wave * PS;
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int mt = 0; mt < MT_MAX; ++mt)
+          if (mt < mtn) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
+          }
+      __syncthreads();
+      if (kpart == 0) {
+#pragma unroll
+        for (int p = 1; p < KSPLIT; ++p) {
+          const float* o = red + (size_t)(wave + p) * PS;
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int mt = 0; mt < MT_MAX; ++mt)
+              if (mt < mtn) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[g][mt][r] += o[((g * MT_MAX + mt) * 4 + r) * 64 + lane];
+              }
+        }
+      }
+      __syncthreads();
+    }
+
+    // ---- epilogue (lane owns column n, rows m = mt*16 + 4*(lane>>4) + r)
+    if (kpart == 0 && active) {
+      const int n = u * 16 + (lane & 15);
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt) {
+        if (mt >= mtn) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = mt * 16 + 4 * (lane >> 4) + r;
+          if (m >= M) continue;
+          if constexpr (EPI == EPI_STORE) {
+            a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
+          } else if constexpr (EPI == EPI_RESID) {
+            bf16_t* p = a.resid + (size_t)m * a.ldo + n;
+            *p = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
+          } else if constexpr (EPI == EPI_SWIGLU) {
+            // unit u = (gate tile, up tile) pair for intermediate columns u*16 .. u*16+15
+            const float gt = rbf(acc[0][mt][r]);
+            const float up = rbf(acc[NG - 1][mt][r]);
+            a.out[(size_t)m * a.ldo + n] = f2bf(rbf(silu_f(gt)) * up);
+          } else if constexpr (EPI == EPI_LOGITS) {
+            float v = rbf(acc[0][mt][r]);  // logits are materialised in bf16, then .float()
+            const uint32_t bits = seen_cur[mt][r];
+            if ((bits >> (n & 31)) & 1u) v = (v < 0.f) ? v * a.penalty : v / a.penalty;
+            if (n == eosr[mt][r]) v = -INFINITY;
+            argmax_merge(best_v[mt][r], best_i[mt][r], v, n);
+          }
+        }
+      }
+    }
+    first = false;
+    if constexpr (EPI == EPI_LOGITS) {
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) seen_cur[mt][r] = seen_nxt[mt][r];
+    }
+  }
+
+  if constexpr (EPI == EPI_LOGITS) {
+    // lanes sharing (lane >> 4) hold the same rows: butterfly over the 16 columns
+#pragma unroll
+    for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float v2 = __shfl_xor(best_v[mt][r], o, 64);
+          const int i2 = __shfl_xor(best_i[mt][r], o, 64);
+          argmax_merge(best_v[mt][r], best_i[mt][r], v2, i2);
+        }
+    // across the unit-groups of the workgroup (only kpart==0 waves hold results)
+    float* rv = red;
+    int* ri = (int*)(red + UPW * MT_MAX * 16);
+    __syncthreads();
+    if (kpart == 0 && (lane & 15) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT_MAX; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = mt * 16 + 4 * (lane >> 4) + r;
+          rv[ugrp * MT_MAX * 16 + m] = best_v[mt][r];
+          ri[ugrp * MT_MAX * 16 + m] = best_i[mt][r];
+        }
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < M; m += NT) {
+      float v = rv[m];
+      int i = ri[m];
+      for (int g = 1; g < UPW; ++g) argmax_merge(v, i, rv[g * MT_MAX * 16 + m], ri[g * MT_MAX * 16 + m]);
+      a.part_val[(size_t)m * a.part_stride + blockIdx.x] = v;
+      a.part_idx[(size_t)m * a.part_stride + blockIdx.x] = i;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host dispatch -------
+// Launch shapes (WAVES, KU, KSPLIT, ring depth R) = the stream plans a matrix can have.
+struct Shape3 { int waves, ku, ksplit, r; bool ng2; };
+inline constexpr Shape3 kShapes[] = {
+    {4, 8, 1, 2, false},    // 0  lm_head
+    {8, 4, 8, 2, false},    // 1  fallback for short K
+    {16, 2, 16, 2, false},  // 2  qkv / o_proj
+    {16, 4, 16, 2, false},  // 3  down
+    {8, 4, 4, 2, true},     // 4  (NG = 2)
+    {8, 2, 4, 2, true},     // 5  gate/up (NG = 2)
+    {16, 2, 8, 2, true},    // 6  (NG = 2)
+};
+inline constexpr int kNumShapes = sizeof(kShapes) / sizeof(kShapes[0]);
+inline bool shape_ng2(int c) { return kShapes[c].ng2; }
+
+template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R, bool EARLY>
+static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
+  const int mt = a.M <= 16 ? 1 : 4;
+  size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
+  lds += (size_t)(WAVES * NG * mt * 4 * 64 + 64) * sizeof(float);
+  if (ASRC == A_ATTN)  // chunk factors (fallback path) or chunk-group partials (early path)
+    lds += std::max((size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit, (size_t)WAVES * 64 * 8) * sizeof(float);
+  if (mt == 1)
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY>), dim3(grid),
+                       dim3(WAVES * 64), lds, s, a);
+  else
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 4, NG, KSPLIT, ASRC, NORM, EPI, R, false>), dim3(grid),
+                       dim3(WAVES * 64), lds, s, a);
+}
+
+// ring depth: the shape's R when it divides the item's stage count S, else 2 or 1
+// early (register-staged) prologue when the rows fit the early registers (decode)
+template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R>
+static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
+  bool early = false;
+  if (a.M <= 16) {
+    const int kch = a.K / 8, NT = WAVES * 64;
+    if (ASRC == A_LDS) early = (kch % 64 == 0) && (a.M * kch + NT - 1) / NT <= wgemm_ea(WAVES);
+    if (ASRC == A_ATTN) early = wgemm_attn_early(a.M, a.K, a.attn_nsplit, WAVES);
+  }
+  if constexpr (ASRC == A_GLOBAL) launch_one_e<WAVES, KU, NG, KSPLIT, ASRC, NORM, EPI, R, false>(a, grid, s);
+  else if (early) launch_one_e<WAVES, KU, NG, KSPLIT, ASRC, NORM, EPI, R, true>(a, grid, s);
+  else launch_one_e<WAVES, KU, NG, KSPLIT, ASRC, NORM, EPI, R, false>(a, grid, s);
+}
+
+template <int C, int NG, int ASRC, bool NORM, int EPI>
+static void launch_shape(const WgemmArgs& a, int grid, hipStream_t s) {
+  constexpr Shape3 h = kShapes[C];
+  const int S = (a.K / 32) / (h.ksplit * h.ku);
+  if (h.r >= 2 && S % 2 == 0) launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 2>(a, grid, s);
+  else launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 1>(a, grid, s);
+}
+
+template <int NG, int ASRC, bool NORM, int EPI>
+static void launch_cfg(const WgemmArgs& a, int cfg, int grid, hipStream_t s) {
+  if constexpr (NG == 2) {
+    switch (cfg) {
+      case 4: launch_shape<4, NG, ASRC, NORM, EPI>(a, grid, s); break;
+      case 6: launch_shape<6, NG, ASRC, NORM, EPI>(a, grid, s); break;
+      default: launch_shape<5, NG, ASRC, NORM, EPI>(a, grid, s); break;
+    }
+  } else {
+    switch (cfg) {
+      case 1: launch_shape<1, NG, ASRC, NORM, EPI>(a, grid, s); break;
+      case 2: launch_shape<2, NG, ASRC, NORM, EPI>(a, grid, s); break;
+      case 3: launch_shape<3, NG, ASRC, NORM, EPI>(a, grid, s); break;
+      default: launch_shape<0, NG, ASRC, NORM, EPI>(a, grid, s); break;
+    }
+  }
+}
+
+// per-epilogue launchers (one translation unit each)
+void launch_wgemm_store(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipStream_t s);
+void launch_wgemm_resid(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipStream_t s);
+void launch_wgemm_swiglu(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipStream_t s);
+void launch_wgemm_logits(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipStream_t s);
+
+}  // namespace tts

@@ -10,13 +10,29 @@ typedef uint16_t bf16_t;
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 
-// Byte range warmed into the Infinity Cache by `wgs` extra workgroups of a launch
-// (prefetch_role in hip_common.h).
-struct Prefetch {
-  const void* ptr = nullptr;
-  size_t bytes = 0;
-  int wgs = 0;
+// Weight layout + decode launch decomposition of one tiled matrix ("stream plan").
+// Work item = (unit of NG n-tiles, K part of KT/ksplit k-tiles); a wave streams its item
+// in stages of ku k-tiles.  Units run in rounds of ur() = grid * waves/ksplit (one unit
+// per wave group of every workgroup).  Tiles are stored round-major, then STAGE-major:
+// at stage s every wave of the launch reads one contiguous block (ur*ksplit*NG*ku KiB),
+// the access pattern that streams HBM fastest (scripts/hbm_floor.hip, pipe sweep).
+struct StreamPlan {
+  int ng = 1, ksplit = 1, ku = 8, waves = 4, grid = 1;
+  __host__ __device__ int ur() const { return grid * (waves / ksplit); }
 };
+// Tile index (1 KiB units) of n-tile nt (unit nt/ng, member nt%ng), k-tile kt.
+__host__ __device__ inline long long plan_tile(int ng, int ksplit, int ku, int ur, int units, int KT,
+                                               int nt, int kt) {
+  const int u = nt / ng, g = nt - u * ng;
+  const int kt_per = KT / ksplit;
+  const int kp = kt / kt_per, ki = kt - kp * kt_per;
+  const int st = ki / ku, kk = ki - st * ku;
+  const int r = u / ur, ui = u - r * ur;
+  const int nr = (units - r * ur) < ur ? (units - r * ur) : ur;
+  return (long long)r * ur * KT * ng +
+         (((long long)st * nr * ksplit + (long long)ui * ksplit + kp) * ng + g) * ku + kk;
+}
+StreamPlan stream_plan(int N, int K, int ng, int num_cu);
 constexpr int LOGITS_MAX_PARTS = 1024;  // lm_head workgroups = argmax partials per row
 
 struct WgemmArgs {
@@ -43,19 +59,22 @@ struct WgemmArgs {
   const float* attn_ml = nullptr;
   const int* attn_pos = nullptr;
   int attn_split = 0, attn_nsplit = 0, attn_D = 0;
-  Prefetch pf;        // cache warming by extra workgroups (set by the engine)
-  int real_grid = 0;  // workgroups doing the GEMM (filled in by launch_wgemm)
+  int ur = 0;         // layout: units per round (StreamPlan::ur, filled in by launch_wgemm)
+  int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
 };
 
 struct WgemmPlan {
-  int cfg = 0;   // launch shape (waves, stage depth, in-workgroup split-K): lm_gemm.hip
+  StreamPlan sp;  // the matrix's layout + launch shape (waves, stage depth, split-K)
+  int cfg = 0;    // kernel instantiation of that shape (lm_gemm.hip)
   int grid = 1;
   bool a_lds = true;
 };
 
-// dest n-tile index = nt * nt_mult + nt_off (nt_mult = 2 interleaves gate/up tiles)
-void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, hipStream_t s, int nt_mult = 1,
-                   int nt_off = 0);
+// Row-major W [N][K] -> tiles of the matrix's stream plan.  The destination matrix has
+// N_total rows; source n-tile nt lands at n-tile nt * nt_mult + nt_off (nt_mult = 2
+// interleaves gate/up n-tiles: unit u = (gate tile u, up tile u), ng = 2).
+void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, int N_total, int ng, int num_cu,
+                   hipStream_t s, int nt_mult = 1, int nt_off = 0);
 WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu);
 bool wgemm_supported(int M, int N, int K, int epi);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
@@ -91,7 +110,6 @@ struct AttnArgs {
   float* part_ml = nullptr; // [rows][H][nsplit][2] (running max, sum)
   bf16_t* q_rot = nullptr;  // prefill: roped q [rows][H*D]
   bf16_t* out = nullptr;    // [rows][H*D] bf16
-  Prefetch pf;              // decode step: cache warming by extra workgroups
 };
 void launch_rope_append(const AttnArgs& a, hipStream_t s);       // prefill: rope q,k; append k,v
 void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);

@@ -150,7 +150,7 @@ def load_library() -> ctypes.CDLL:
         "tts_codec_decode": (I32, [P, pi32, pi32, I32, P, I32, ctypes.POINTER(ctypes.c_int64), P]),
         "tts_codec_samples_per_code": (I32, [P, pi32]),
         "tts_synth_fill": (I32, [P, I32, I64, U64, F32, P]),
-        "tts_op_retile": (I32, [P, P, I32, I32, P]),
+        "tts_op_retile": (I32, [P, P, I32, I32, I32, P]),
         "tts_op_wgemm": (I32, [P, I32, I32, I32, P, I32, P, F32, P, I32, P, I32, P]),
         "tts_op_rmsnorm": (I32, [P, P, F32, P, I32, I32, P]),
         "tts_op_gemm_f32": (I32, [P, I32, I32, I32, P, I32, P, P, I32, P, I32, P]),
