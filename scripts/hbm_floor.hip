@@ -116,17 +116,17 @@ int main() {
   }
 
   // ---- pattern sweep
-  for (double mb : {12.582912, 67.108864, 794.034176}) {
+  for (double mb : {8.388608, 12.582912, 33.554432, 67.108864}) {
     const size_t bytes = (size_t)(mb * 1e6);
     const size_t tiles = bytes / 1024;
     const int copies = (int)(pool / bytes) > 16 ? 16 : (int)(pool / bytes);
     for (int waves : {4, 8, 16}) {
-      for (int grid : {256, 512}) {
+      for (int grid : {128, 192, 256}) {
         const int nw = grid * waves;
-        for (int ku : {2, 4, 8, 16}) {
+        for (int ku : {2, 4}) {
           if (tiles % ((size_t)nw * ku)) continue;
           const int tpw = (int)(tiles / nw);
-          for (int pat = 0; pat < 2; ++pat) {
+          for (int pat = 1; pat < 2; ++pat) {
             auto launch = [&](int c) {
               const u32x4_t* p = (const u32x4_t*)(buf + (size_t)c * bytes);
 #define P(KU, PT) hipLaunchKernelGGL((pipe_kernel<KU, PT>), dim3(grid), dim3(waves * 64), 0, 0, p, tpw, sink)

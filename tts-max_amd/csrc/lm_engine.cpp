@@ -260,6 +260,14 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
 // ------------------------------------------------------------------------ compute -----
 namespace {
 
+// Decode attention form: chunked kernel (32 workgroups per row at 450 positions) whose
+// partials the o_proj prologue merges (default), or one workgroup per (row, kv head) that
+// merges in LDS (TTS_ATTN_MERGED=1; measured 2x slower at batch 1: 8 CUs stream the KV).
+bool use_split_attn() {
+  static const bool v = !(getenv("TTS_ATTN_MERGED") && atoi(getenv("TTS_ATTN_MERGED")));
+  return v;
+}
+
 struct Ctx {
   Engine* e;
   hipStream_t s;
@@ -322,10 +330,14 @@ struct Ctx {
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(),
            nullptr, EPI_STORE);
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
-      // decode with few rows: the o_proj prologue merges the attention chunks itself
-      const bool fuse_combine = decode && rows <= kPrefillChunk &&
+      // decode: one workgroup per (row, kv head) attends and merges (default), or the
+      // chunked kernel whose partials the o_proj prologue merges (TTS_ATTN_SPLIT=1)
+      const bool split_attn = use_split_attn();
+      const bool fuse_combine = decode && split_attn && rows <= kPrefillChunk &&
                                 plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
-      if (decode) {
+      if (decode && !split_attn) {
+        launch_attn_decode_merged(a, s);
+      } else if (decode) {
         launch_attn_decode_step(a, s);
       } else {
         launch_rope_append(a, s);
@@ -337,7 +349,7 @@ struct Ctx {
         exo.attn_split = a.split; exo.attn_nsplit = a.nsplit; exo.attn_D = a.D;
         gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &exo);
       } else {
-        launch_attn_combine(a, s);
+        if (!decode || split_attn) launch_attn_combine(a, s);
         gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
              w.x.as<bf16_t>(), EPI_RESID);
       }
@@ -564,7 +576,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   ex.part_stride = LOGITS_MAX_PARTS;
   // attention chunk partials for the fused o_proj prologue
   launch_attn_decode_step(aa, s);
-  const bool fuse_o = plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
+  const bool fuse_o = use_split_attn() && plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
   WgemmArgs exo;
   exo.attn_o = aa.part_o; exo.attn_ml = aa.part_ml; exo.attn_pos = e->w.row_pos.as<int>();
   exo.attn_split = aa.split; exo.attn_nsplit = aa.nsplit; exo.attn_D = aa.D;
@@ -603,7 +615,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         b = 2.0 * V * HID + act_rw * HID + 2.0 * HID + rows * (V / 8.0);
         break;
       case 5:
-        launch_attn_decode_step(aa, s);
+        if (use_split_attn()) launch_attn_decode_step(aa, s);
+        else launch_attn_decode_merged(aa, s);
         b = (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2 + act_rw * QKV;
         break;
     }

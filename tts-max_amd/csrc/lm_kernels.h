@@ -116,6 +116,9 @@ void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
 // decode step: register-streamed chunks of decode_split(D) positions, KV append fused
 int decode_split(int D);
 void launch_attn_decode_step(const AttnArgs& a, hipStream_t s);
+// decode step, one workgroup per (row, kv head): RoPE + KV append + attention + merge,
+// bf16 output in a.out [rows][H*D]
+void launch_attn_decode_merged(const AttnArgs& a, hipStream_t s);
 void launch_attn_combine(const AttnArgs& a, hipStream_t s);
 
 // ---- sampling / bookkeeping (lm_ops.hip)
