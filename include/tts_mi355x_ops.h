@@ -32,6 +32,13 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
                         int32_t N, const void* normw, float eps, void* out, int32_t ldo,
                         void* resid, int32_t epi, void* stream);
 
+/* Prefill GEMM (many rows, one launch): same tiled weights and epilogues as tts_op_wgemm
+ * (0 store, 1 residual, 2 SwiGLU), no fused RMSNorm, any M >= 1; N % 64 == 0, K % 64 == 0.
+ * Replaces the per-token projections of transformers LlamaForCausalLM.forward over the
+ * prompt (modeling_llama.py:163-176, 217-281) when the whole prompt batch is prefilled. */
+tts_status tts_op_pgemm(const void* x, int32_t M, int32_t K, const void* w_tiled, int32_t N, void* out,
+                        int32_t ldo, void* resid, int32_t epi, void* stream);
+
 /* LlamaRMSNorm over rows of x (bf16). */
 tts_status tts_op_rmsnorm(const void* x, const void* w, float eps, void* y, int32_t M, int32_t K,
                           void* stream);

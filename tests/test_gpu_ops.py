@@ -155,3 +155,72 @@ def test_gemm_f32_sliding_window_conv(lib):
                                None, 0, None))
     torch.cuda.synchronize()
     assert torch.allclose(out.cpu(), ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("M", [16, 24, 32, 40, 64])
+@pytest.mark.parametrize("N,K,epi", [(3072, 2048, 0), (2048, 8192, 1), (2048, 2048, 1), (16384, 2048, 2)])
+def test_wgemm_rows_independent(lib, M, N, K, epi):
+    """Rows never mix: M copies of one activation row give M identical output rows, whatever
+    launch form the row count selects (A in LDS or global, K-sliced, 1/2/4 m-tiles)."""
+    g = torch.Generator().manual_seed(N + K + epi)
+    x1 = (torch.randn(1, K, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.02).to(torch.bfloat16)
+    nw = (1 + 0.2 * torch.randn(K, generator=g)).to(torch.bfloat16) if epi != 1 and M <= 32 else None
+    xd = x1.repeat(M, 1).cuda()
+    wt = _tiled(lib, w.cuda(), epi=epi)
+    nout = N // 2 if epi == 2 else N
+    out = torch.zeros(M, nout, dtype=torch.bfloat16, device="cuda")
+    res = (torch.randn(1, N, generator=g) * 0.5).to(torch.bfloat16).repeat(M, 1).cuda() if epi == 1 else None
+    _check(lib.tts_op_wgemm(xd.data_ptr(), M, K, K, wt.data_ptr(), N, nw.cuda().data_ptr() if nw is not None else None,
+                            1e-5, out.data_ptr() if epi != 1 else None, nout,
+                            res.data_ptr() if res is not None else None, epi, None))
+    torch.cuda.synchronize()
+    y = (res if epi == 1 else out).cpu()
+    assert torch.equal(y, y[:1].expand_as(y)), [int((y[i] != y[0]).sum()) for i in range(M)]
+
+
+@pytest.mark.parametrize("M", [65, 202, 700])
+@pytest.mark.parametrize("N,K", [(384, 256), (3072, 2048), (2048, 8192)])
+def test_pgemm_store_and_rows_independent(lib, M, N, K):
+    """Prefill GEMM (tiles of the decode stream-plan layout, LDS-staged MFMA blocks) against
+    the oracle's bf16 nn.Linear; the first and last rows are copies, so they must agree bit
+    for bit whatever row block they fall in."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16)
+    x[-1] = x[0]
+    w = (torch.randn(N, K, generator=g) * 0.02).to(torch.bfloat16)
+    ref = lm_oracle.linear(x, w)
+    wt = _tiled(lib, w.cuda())
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    _check(lib.tts_op_pgemm(x.cuda().data_ptr(), M, K, wt.data_ptr(), N, out.data_ptr(), N, None, 0, None))
+    torch.cuda.synchronize()
+    o = out.cpu()
+    _bf16_close(o, ref)
+    assert torch.equal(o[0], o[-1])
+
+
+@pytest.mark.parametrize("M", [130, 600])
+def test_pgemm_resid_swiglu(lib, M):
+    K, FF = 2048, 1024
+    g = torch.Generator().manual_seed(M)
+    h = (torch.randn(M, K, generator=g)).to(torch.bfloat16)
+    wg = (torch.randn(FF, K, generator=g) * 0.02).to(torch.bfloat16)
+    wu = (torch.randn(FF, K, generator=g) * 0.02).to(torch.bfloat16)
+    ref_act = torch.nn.functional.silu(lm_oracle.linear(h, wg)) * lm_oracle.linear(h, wu)
+    wgu = _tiled(lib, torch.cat([wg, wu]).cuda(), epi=2)
+    act = torch.empty(M, FF, dtype=torch.bfloat16, device="cuda")
+    _check(lib.tts_op_pgemm(h.cuda().data_ptr(), M, K, wgu.data_ptr(), 2 * FF, act.data_ptr(), FF, None, 2, None))
+    torch.cuda.synchronize()
+    _bf16_close(act.cpu(), ref_act, max_ulps=3, frac=0.03)
+    wd = (torch.randn(K, FF, generator=g) * 0.02).to(torch.bfloat16)
+    ref_res = h + lm_oracle.linear(ref_act, wd)
+    res = h.cuda()
+    a = ref_act.cuda()
+    _check(lib.tts_op_pgemm(a.data_ptr(), M, FF, _tiled(lib, wd.cuda()).data_ptr(), K, None, K, res.data_ptr(), 1, None))
+    torch.cuda.synchronize()
+    # residual add: an ulp of the projection is an ulp of max(|h|, |y|), not of the
+    # (possibly cancelled) sum
+    y = lm_oracle.linear(ref_act, wd).float()
+    scale = torch.maximum(h.float().abs(), y.abs())
+    err = (res.cpu().float() - ref_res.float()).abs()
+    assert (err > 4 * scale * 2.0 ** -8 + 1e-6).sum().item() == 0

@@ -213,14 +213,34 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
     TTS_REQUIRE(wgemm_supported(M, N, K, epi), "unsupported GEMM shape");
     TTS_REQUIRE(ldx == K, "ldx must equal K");
     WgemmPlan p = plan_wgemm(M, N, K, epi, device_cu_count());
-    TTS_REQUIRE(normw == nullptr || (p.a_lds && K <= 4096),
+    TTS_REQUIRE(normw == nullptr || (p.a_lds && !p.sliced && K <= 4096),
                 "fused RMSNorm needs M*K small enough for LDS and K <= 4096");
     WgemmArgs a;
     a.x = (const bf16_t*)x; a.M = M; a.K = K; a.ldx = ldx;
     a.w = (const bf16_t*)w_tiled; a.N = N;
     a.normw = (const bf16_t*)normw; a.eps = eps;
     a.out = (bf16_t*)out; a.ldo = ldo; a.resid = (bf16_t*)resid;
-    launch_wgemm(a, p, epi, normw != nullptr, (hipStream_t)stream);
+    float* part = nullptr;
+    if (p.sliced) {
+      HIP_CHECK(hipMallocAsync((void**)&part, wgemm_part_elems(p, M, ldo) * 4, (hipStream_t)stream));
+      a.part_out = part;
+    }
+    launch_wgemm(a, p, epi, normw != nullptr && !p.sliced, (hipStream_t)stream);
+    HIP_CHECK(hipGetLastError());
+    if (part) HIP_CHECK(hipFreeAsync(part, (hipStream_t)stream));
+  });
+}
+
+tts_status tts_op_pgemm(const void* x, int32_t M, int32_t K, const void* w_tiled, int32_t N, void* out,
+                        int32_t ldo, void* resid, int32_t epi, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(pgemm_supported(M, N, K, epi), "unsupported prefill GEMM shape / epilogue");
+    TTS_REQUIRE(epi == EPI_RESID ? resid != nullptr : out != nullptr, "missing output");
+    PgemmArgs a;
+    a.x = (const bf16_t*)x; a.M = M; a.K = K; a.ldx = K;
+    a.w = (const bf16_t*)w_tiled; a.N = N;
+    a.out = (bf16_t*)out; a.ldo = ldo; a.resid = (bf16_t*)resid;
+    launch_pgemm(a, epi, device_cu_count(), (hipStream_t)stream);
     HIP_CHECK(hipGetLastError());
   });
 }

@@ -84,6 +84,7 @@ struct LmWork {
   DevBuf x, xn, qkv, attn_out, act, q_rot, last_x;  // activations
   DevBuf part_o, part_ml;                           // attention split partials
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
+  DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf logits;                                    // scoring output (bf16)
   DevBuf row_slot, row_pos, row_idx;                // prefill row descriptors
   DevBuf st_int;                                    // step-state ints

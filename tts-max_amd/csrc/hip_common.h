@@ -16,18 +16,17 @@ TTS_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 TTS_DEV float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 TTS_DEV float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// fp32 -> bf16 round-to-nearest-even, NaN preserved (same rounding as torch's .to(bfloat16)).
-TTS_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// fp32 -> bf16 round-to-nearest-even (same rounding as torch's .to(bfloat16)): gfx950's
+// v_cvt_pk_bf16_f32.  (A software RNE with a NaN test compiles to an exec-mask branch per
+// element: ~25 instructions, which made the RMSNorm prologues the cost of a whole GEMV.)
+typedef __attribute__((ext_vector_type(2))) float f32x2_cvt_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_cvt_t;
+TTS_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 // Round an fp32 value to the nearest bf16 value, returned as fp32 (torch bf16 op semantics:
 // every bf16 elementwise op computes in fp32 and rounds its result once).
 TTS_DEV float rbf(float f) { return bf2f(f2bf(f)); }
 TTS_DEV uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_cvt_t){lo, hi}, bf16x2_cvt_t));
 }
 
 // ---- DPP wave reductions (VALU speed; __shfl_xor lowers to ds_bpermute = LDS latency)
@@ -46,6 +45,25 @@ TTS_DEV float wave_sum_dpp(float v) {
   v += dpp_mov<0x142, 0xA>(0.f, v);
   v += dpp_mov<0x143, 0xC>(0.f, v);
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// LDS-DMA operand pointer types (__builtin_amdgcn_global_load_lds)
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int waitcnt_vm(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | (7 << 4) | (15 << 8); }
+constexpr int waitcnt_lgkm0() { return 15 | (3 << 14) | (7 << 4); }
+
+// RMSNorm sum of squares, canonical order shared by every implementation (fused prologue,
+// LDS prologue, standalone kernel) so all of them round identically: per 16-B chunk of 8
+// values, then a DPP wave sum over each 512-value segment, then the segments in order.
+TTS_DEV float chunk_sumsq(u32x4_t v) {
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float lo = bf_lo(v[q]), hi = bf_hi(v[q]);
+    s += lo * lo + hi * hi;
+  }
+  return s;
 }
 TTS_DEV float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_mov<0xB1>(-INFINITY, v));

@@ -244,6 +244,10 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
       std::max((size_t)R * w.nsplit_prefill, (size_t)B * w.nsplit_decode);
   w.part_o.alloc(part_rows * H * D * 4);
   w.part_ml.alloc(part_rows * H * 2 * 4);
+  {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
+    const int kmax = std::max(HID, std::max(FF, H * D));
+    w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
+  }
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.row_slot.alloc((size_t)R * 4);
@@ -281,12 +285,26 @@ struct Ctx {
   // out = epi(x . W^T) over M rows (chunked by 64), RMSNorm prologue if normw != nullptr.
   void gemm(const bf16_t* x, int rows, int K, const bf16_t* W, int N, const bf16_t* normw,
             bf16_t* out, int ldo, bf16_t* resid, int epi, const WgemmArgs* logit_extra = nullptr) {
+    if (rows > kPrefillChunk && x && pgemm_supported(rows, N, K, epi)) {
+      // prefill: every prompt row of the batch in one LDS-staged MFMA launch
+      const bf16_t* xin = x;
+      if (normw) {
+        launch_rmsnorm(x, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, rows, K, s);
+        xin = w.xn.as<bf16_t>();
+      }
+      PgemmArgs a;
+      a.x = xin; a.M = rows; a.K = K; a.ldx = K;
+      a.w = W; a.N = N;
+      a.out = out; a.ldo = ldo; a.resid = resid;
+      launch_pgemm(a, epi, e->num_cu, s);
+      return;
+    }
     for (int r0 = 0; r0 < rows; r0 += kPrefillChunk) {
       const int m = std::min(kPrefillChunk, rows - r0);
       WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
       const bf16_t* xin = x ? x + (size_t)r0 * K : nullptr;
       bool norm = normw != nullptr;
-      if (norm && (!p.a_lds || K > 4096)) {  // fused RMSNorm: rows in LDS, K <= 4096
+      if (norm && (!p.a_lds || p.sliced || K > 4096)) {  // fused RMSNorm: rows in LDS, K <= 4096
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
@@ -298,6 +316,10 @@ struct Ctx {
       a.normw = normw; a.eps = c.rms_norm_eps;
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
+      if (p.sliced) {
+        TTS_REQUIRE(wgemm_part_elems(p, m, ldo) * 4 <= w.kpart.bytes, "K-sliced partial workspace too small");
+        a.part_out = w.kpart.as<float>();
+      }
       launch_wgemm(a, p, epi, norm, s);
     }
   }
@@ -333,7 +355,8 @@ struct Ctx {
       // decode: one workgroup per (row, kv head) attends and merges (default), or the
       // chunked kernel whose partials the o_proj prologue merges (TTS_ATTN_SPLIT=1)
       const bool split_attn = use_split_attn();
-      const bool fuse_combine = decode && split_attn && rows <= kPrefillChunk &&
+      // (rows <= 16: the merge scratch + A rows fit LDS beside the split-K partials)
+      const bool fuse_combine = decode && split_attn && rows <= 16 &&
                                 plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
       if (decode && !split_attn) {
         launch_attn_decode_merged(a, s);
@@ -576,7 +599,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   ex.part_stride = LOGITS_MAX_PARTS;
   // attention chunk partials for the fused o_proj prologue
   launch_attn_decode_step(aa, s);
-  const bool fuse_o = use_split_attn() && plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
+  const bool fuse_o = use_split_attn() && rows <= 16 && plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
   WgemmArgs exo;
   exo.attn_o = aa.part_o; exo.attn_ml = aa.part_ml; exo.attn_pos = e->w.row_pos.as<int>();
   exo.attn_split = aa.split; exo.attn_nsplit = aa.nsplit; exo.attn_D = aa.D;

@@ -42,7 +42,7 @@ __global__ void retile_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__
     const int n = nt * 16 + (lane & 15);
     const int k = kt * 32 + 8 * (lane >> 4);
     const u32x4_t v = *(const u32x4_t*)(w + (size_t)n * K + k);
-    const long long dtile = plan_tile(p.ng, p.ksplit, p.ku, ur, units, KT, nt * nt_mult + nt_off, kt);
+    const long long dtile = plan_tile(p.ng, p.ksplit, p.ku, ur, units, KT, p.kc, nt * nt_mult + nt_off, kt);
     *(u32x4_t*)(t + (size_t)(dtile * 64 + lane) * 8) = v;
   }
 }
@@ -98,6 +98,9 @@ StreamPlan stream_plan(int N, int K, int ng, int num_cu) {
   // EPI_LOGITS hold at most LOGITS_MAX_PARTS workgroups
   const int cap = (fgrid > 0) ? std::min(fgrid, LOGITS_MAX_PARTS) : num_cu;
   p.grid = std::min(grid, cap);
+  // K chunks of 2048 columns (64 k-tiles) where the shape divides them: at batch 17..32 one
+  // chunk of A (32 x 2048 bf16 = 128 KiB) fits LDS where the whole K (8192) does not
+  if (K > 2048 && K % 2048 == 0 && (2048 / 32) % (p.ksplit * p.ku) == 0) p.kc = K / 2048;
   return p;
 }
 
@@ -109,13 +112,30 @@ static int shape_index(const StreamPlan& p) {
   return -1;
 }
 
+// LDS of one launch: A rows (+16 B per row), split-K partials of the waves with kpart > 0,
+// the argmax / RMSNorm-segment scratch, and 64 floats of slack.  Must match the kernel's
+// carve-up (wgemm_kernel: red_floats).
+size_t wgemm_lds_bytes(int waves, int ksplit, int ng, int M, int Kl, bool a_in_lds) {
+  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  const size_t xs = a_in_lds ? (((size_t)M * (Kl + 8) * 2 + 15) & ~(size_t)15) : 0;
+  return xs + (size_t)wgemm_red_floats(waves, ksplit, ng, mt, M, Kl) * sizeof(float);
+}
+
+static constexpr size_t kLdsBudget = 160 * 1024;
+
 WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   WgemmPlan p;
   const int ng = (epi == EPI_SWIGLU) ? 2 : 1;
   p.sp = stream_plan(N, K, ng, num_cu);
   p.cfg = shape_index(p.sp);
   p.grid = p.sp.grid;
-  p.a_lds = ((size_t)M * (K + 8) * 2) <= 80 * 1024;
+  const int w = p.sp.waves, ks = p.sp.ksplit;
+  p.a_lds = wgemm_lds_bytes(w, ks, ng, M, K, true) <= kLdsBudget;
+  if (!p.a_lds && p.sp.kc > 1 && (epi == EPI_STORE || epi == EPI_RESID) &&
+      wgemm_lds_bytes(w, ks, ng, M, K / p.sp.kc, true) <= kLdsBudget) {
+    p.a_lds = true;
+    p.sliced = true;
+  }
   return p;
 }
 
@@ -127,8 +147,23 @@ bool wgemm_supported(int M, int N, int K, int epi) {
 void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p, int epi, bool norm, hipStream_t s) {
   WgemmArgs a = a_in;
   a.ur = p.sp.ur();
+  a.kc = p.sp.kc;
+  a.sliced = p.sliced ? 1 : 0;
   static const int diag = getenv("TTS_WGEMM_DIAG") ? atoi(getenv("TTS_WGEMM_DIAG")) : 0;
   a.diag = diag;
+  if (p.sliced) {
+    // one K chunk per workgroup row of the grid: fp32 partials, then the epilogue in a
+    // combine kernel (fixed chunk order: deterministic)
+    if (norm || (epi != EPI_STORE && epi != EPI_RESID) || a.part_out == nullptr)
+      throw std::runtime_error("K-sliced wgemm: store/residual epilogues with a partial workspace only");
+    const int Kfull = a.K;
+    a.K = Kfull / p.sp.kc;  // the kernel's A chunk; ldx stays the full row
+    launch_wgemm_store(a, p, false, s);
+    launch_splitk_combine(a.part_out, p.sp.kc, a.M, a.N, a.ldo, a.out, epi == EPI_RESID ? a.resid : nullptr,
+                          a.ldo, s);
+    return;
+  }
+  a.part_out = nullptr;
   switch (epi) {
     case EPI_STORE: launch_wgemm_store(a, p, norm, s); break;
     case EPI_RESID: launch_wgemm_resid(a, p, norm, s); break;

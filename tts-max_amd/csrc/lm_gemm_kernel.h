@@ -14,6 +14,17 @@ namespace tts {
 // register budget of the early prologue: A chunks per thread / attention chunks per group
 constexpr int wgemm_ea(int waves) { return waves >= 16 ? 1 : (waves >= 8 ? 2 : 4); }
 constexpr int wgemm_cpg(int waves) { return waves >= 16 ? 2 : 4; }
+// floats of the kernel's scratch region `red`: split-K partials of the waves with kpart > 0,
+// the lm_head argmax exchange, the early RMSNorm segment sums (+64 slack)
+__host__ __device__ inline int wgemm_red_floats(int waves, int ksplit, int ng, int mt, int M, int Kl) {
+  const int upw = waves / ksplit;
+  int r = upw * (ksplit - 1) * ng * mt * 4 * 64;
+  r = r > upw * mt * 16 * 2 ? r : upw * mt * 16 * 2;
+  const int segs = (M * (Kl / 8) + 63) / 64;
+  r = r > segs ? r : segs;
+  r = r > Kl / 2 ? r : Kl / 2;  // RMSNorm weight (bf16) parked here during the LDS-DMA prologue
+  return r + 64;
+}
 #define WGEMM_NSX 8
 inline bool wgemm_attn_early(int M, int K, int nsplit, int waves) {
   const int aitems = M * (K / 8), NT = waves * 64;
@@ -51,18 +62,25 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   const int ugrp = wave / KSPLIT;
   const int M = a.M;
   const int mtn = (M + 15) >> 4;
-  const int KT = a.K >> 5;
   const int units = (a.N >> 4) / NG;
-  const int kt_per = KT / KSPLIT;
-  const int kt0 = kpart * kt_per;
-  const int kend = kt0 + kt_per;
+  // K layout (StreamPlan::kc chunks, chunk-major): a wave's K part is kt_pc k-tiles of every
+  // chunk; its stage st covers k-tiles kt(st) .. +KU-1 of chunk st / Sc.  K-sliced launches
+  // (a.sliced) run chunk blockIdx.y only: a.K = one chunk, A = that chunk's columns.
+  const int kc = a.kc;
+  const int KT = a.sliced ? (a.K >> 5) * kc : (a.K >> 5);  // k-tiles of the whole matrix
+  const int KTc = KT / kc;
+  const int kt_pc = KTc / KSPLIT;
+  const int Sc = kt_pc / KU;
+  const int st_off = a.sliced ? blockIdx.y * Sc : 0;        // first (layout) stage of this launch
+  const int kt_base = a.sliced ? blockIdx.y * KTc : 0;      // first k-tile held in A
+  const bf16_t* xg = a.x ? a.x + (a.sliced ? (size_t)blockIdx.y * a.K : 0) : nullptr;
   const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
   const int ustride = gridDim.x * UPW;
 
   bf16_t* xs = (bf16_t*)smem;
   const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
-  float* red = (float*)(smem + xs_bytes);  // [WAVES][NG*MT_MAX*4][64] split-K partials
-  float* xtra = red + WAVES * NG * MT_MAX * 4 * 64 + 64;  // A_ATTN scratch
+  float* red = (float*)(smem + xs_bytes);  // split-K partials of waves kpart > 0, scratch
+  float* xtra = red + wgemm_red_floats(WAVES, KSPLIT, NG, MT_MAX, M, a.K);  // A_ATTN scratch
 
   // ---- operands of the prologue and epilogue are loaded FIRST, the weight stream after:
   // vmcnt retires in issue order, so anything issued behind the stream could not be used
@@ -81,8 +99,30 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int j = 0; j < EA; ++j) {  // all EA issued (clamped): a fixed load count keeps the
         const int c = min(tid + j * NT, achunks - 1);  // vmcnt waits below exact
         const int m = c / kch, k = (c - m * kch) * 8;
-        xe[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+        xe[j] = *(const u32x4_t*)(xg + (size_t)m * a.ldx + k);
         if constexpr (NORM) ne[j] = *(const u32x4_t*)(a.normw + k);
+      }
+    }
+  }
+  // (a') rows too many for the early registers: LDS-DMA (global_load_lds, 1 KiB per wave
+  //      instruction, one row piece each) straight into the padded LDS rows, and the RMSNorm
+  //      weight into the (still unused) split-K scratch — no VGPRs, and issued ahead of the
+  //      weight stream like every other operand
+  constexpr bool glds_ok = ASRC == A_LDS && !early_a;
+  const bool use_glds = glds_ok && (a.K & 511) == 0;
+  if constexpr (glds_ok) {
+    if (use_glds) {
+      const int ppr = a.K >> 9;
+      const int pieces = M * ppr;
+      for (int p = wave; p < pieces; p += WAVES) {
+        const int m = p / ppr, kp = p - m * ppr;
+        __builtin_amdgcn_global_load_lds((gptr_t)(xg + (size_t)m * a.ldx + kp * 512 + lane * 8),
+                                         (lptr_t)(xs + (size_t)m * ldxs + kp * 512), 16, 0, 0);
+      }
+      if constexpr (NORM) {
+        for (int p = wave; p < ppr; p += WAVES)
+          __builtin_amdgcn_global_load_lds((gptr_t)(a.normw + p * 512 + lane * 8), (lptr_t)((bf16_t*)red + p * 512),
+                                           16, 0, 0);
       }
     }
   }
@@ -142,13 +182,14 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     uu = min(uu, units - 1);
     const int r = uu / ur, ui = uu - r * ur;
     const int nr = min(ur, units - r * ur);
-    const long long t = (long long)r * ur * KT * NG + (((long long)st * nr + ui) * KSPLIT + kpart) * NG * KU;
+    const long long t =
+        (long long)r * ur * KT * NG + (((long long)(st + st_off) * nr + ui) * KSPLIT + kpart) * NG * KU;
     return (const u32x4_t*)a.w + t * 64 + lane;
   };
   // Register ring of R stages (S = stages per item, S % R == 0): the first R stages of the
   // wave's stream are in flight before the prologue runs; consuming a slot refills it with
   // the stage R positions later (next unit's stages once this unit's are all issued).
-  const int S = kt_per / KU;
+  const int S = a.sliced ? Sc : kc * Sc;  // stages per item in this launch
   u32x4_t wr[R][KU][NG];
   int pu = u, ps = 0;  // next stage to issue
   // The refills are issued only where the stage exists by construction (never behind a
@@ -184,13 +225,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
       for (int j = 0; j < EA; ++j) {
         if (j < a_nj) {
-          float s = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = bf_lo(xe[j][q]), hi = bf_hi(xe[j][q]);
-            s += lo * lo + hi * hi;
-          }
-          s = wave_sum_dpp(s);
+          const float s = wave_sum_dpp(chunk_sumsq(xe[j]));
           const int c = tid + j * NT;
           if (lane == 0 && c < achunks) red[c >> 6] = s;
         }
@@ -221,16 +256,54 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
     __syncthreads();
+   } else if (use_glds) {
+    // rows landed by LDS-DMA: wait for this wave's DMA only (the weight ring issued after
+    // it stays in flight), then every wave's (raw barrier: __syncthreads would drain the ring)
+    if (!(a.diag & 32)) {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(R * KU * NG));
+      __builtin_amdgcn_s_barrier();
+    }
+    if (a.diag & 16) {
+    } else if constexpr (NORM) {
+      const bf16_t* gw = (const bf16_t*)red;
+      for (int m = wave; m < M; m += WAVES) {
+        bf16_t* xr = xs + (size_t)m * ldxs;
+        float ss = 0.f;
+        for (int k0 = 0; k0 < a.K; k0 += 512)  // canonical order (chunk_sumsq)
+          ss += wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xr + k0 + lane * 8)));
+        const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+        for (int k = lane * 8; k < a.K; k += 512) {
+          u32x4_t v = *(const u32x4_t*)(xr + k);
+          const u32x4_t g = *(const u32x4_t*)(gw + k);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+          *(u32x4_t*)(xr + k) = v;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
+      __builtin_amdgcn_s_barrier();
+    }
    } else {
     // general rows (more than the early registers hold): 16-B copies into LDS, 4 per
-    // thread in flight (clamped, unconditional loads), then RMSNorm in place, a wave per row
+    // thread in flight (clamped, unconditional loads), then RMSNorm in place, a wave per row.
+    // The lane's RMSNorm weight chunks (k = lane*8 + 512 i) ride with the first copy batch:
+    // loaded inside the per-row loop they would be a chain of dependent L2 round trips.
+    constexpr int NKX = 8;  // K <= 4096 (host: fused RMSNorm only up to K = 4096)
+    u32x4_t gw[NORM ? NKX : 1];
     for (int c0 = 0; c0 < achunks; c0 += 4 * NT) {
       u32x4_t v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = min(c0 + tid + j * NT, achunks - 1);
         const int m = c / kch, k = (c - m * kch) * 8;
-        v[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+        v[j] = *(const u32x4_t*)(xg + (size_t)m * a.ldx + k);
+      }
+      if constexpr (NORM) {
+        if (c0 == 0) {
+#pragma unroll
+          for (int i = 0; i < NKX; ++i) gw[i] = *(const u32x4_t*)(a.normw + min(lane * 8 + i * 512, a.K - 8));
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -246,23 +319,23 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int m = wave; m < M; m += WAVES) {
         bf16_t* xr = xs + (size_t)m * ldxs;
         float ss = 0.f;
-        for (int k = lane * 8; k < a.K; k += 512) {
-          const u32x4_t v = *(const u32x4_t*)(xr + k);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = bf_lo(v[q]), hi = bf_hi(v[q]);
-            ss += lo * lo + hi * hi;
-          }
+        for (int k0 = 0; k0 < a.K; k0 += 512) {  // canonical order (chunk_sumsq)
+          const int k = k0 + lane * 8;
+          const float s = k < a.K ? chunk_sumsq(*(const u32x4_t*)(xr + k)) : 0.f;
+          ss += wave_sum_dpp(s);
         }
-        ss = wave_sum_dpp(ss);
         const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-        for (int k = lane * 8; k < a.K; k += 512) {
-          u32x4_t v = *(const u32x4_t*)(xr + k);
-          const u32x4_t g = *(const u32x4_t*)(a.normw + k);
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
-          *(u32x4_t*)(xr + k) = v;
+        for (int i = 0; i < NKX; ++i) {
+          const int k = lane * 8 + i * 512;
+          if (k < a.K) {
+            u32x4_t v = *(const u32x4_t*)(xr + k);
+            const u32x4_t g = gw[i];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+            *(u32x4_t*)(xr + k) = v;
+          }
         }
       }
     }
@@ -393,7 +466,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     auto consume = [&](const u32x4_t (&src)[KU][NG], int stage) {
-      const int kt = kt0 + stage * KU;
+      const int sg = stage + st_off, ch = kc == 1 ? 0 : sg / Sc;
+      const int kt = ch * KTc + kpart * kt_pc + (sg - ch * Sc) * KU - kt_base;  // A column tile
 #pragma unroll
       for (int kk = 0; kk < KU; ++kk) {
         const int k = (kt + kk) * 32 + akoff;
@@ -402,7 +476,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           const int m = min(mt * 16 + arow, M - 1);  // rows >= M: duplicates, never stored
           u32x4_t av;
           if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
-          else av = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + k);
+          else av = *(const u32x4_t*)(xg + (size_t)m * a.ldx + k);
           const bf16x8_t af = as_bf16x8(av);
 #pragma unroll
           for (int g = 0; g < NG; ++g)
@@ -431,21 +505,24 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
     // ---- split-K combine through LDS, fixed order (deterministic)
     if constexpr (KSPLIT > 1) {
+      // slot of wave (ugrp, kpart > 0): ugrp * (KSPLIT-1) + kpart - 1
       constexpr int PS = NG * MT_MAX * 4 * 64;
-      float* myred = red + (size_t)wave * PS;
+      if (kpart > 0) {
+        float* myred = red + (size_t)(ugrp * (KSPLIT - 1) + kpart - 1) * PS;
 #pragma unroll
-      for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NG; ++g)
 #pragma unroll
-        for (int mt = 0; mt < MT_MAX; ++mt)
-          if (mt < mtn) {
+          for (int mt = 0; mt < MT_MAX; ++mt)
+            if (mt < mtn) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
-          }
+              for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
+            }
+      }
       __syncthreads();
       if (kpart == 0) {
 #pragma unroll
         for (int p = 1; p < KSPLIT; ++p) {
-          const float* o = red + (size_t)(wave + p) * PS;
+          const float* o = red + (size_t)(ugrp * (KSPLIT - 1) + p - 1) * PS;
 #pragma unroll
           for (int g = 0; g < NG; ++g)
 #pragma unroll
@@ -470,7 +547,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           const int m = mt * 16 + 4 * (lane >> 4) + r;
           if (m >= M) continue;
           if constexpr (EPI == EPI_STORE) {
-            a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
+            if (a.part_out) a.part_out[((size_t)blockIdx.y * M + m) * a.ldo + n] = acc[0][mt][r];
+            else a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
           } else if constexpr (EPI == EPI_RESID) {
             bf16_t* p = a.resid + (size_t)m * a.ldo + n;
             *p = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
@@ -552,16 +630,21 @@ inline bool shape_ng2(int c) { return kShapes[c].ng2; }
 
 template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R, bool EARLY>
 static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
-  const int mt = a.M <= 16 ? 1 : 4;
+  const int mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
-  lds += (size_t)(WAVES * NG * mt * 4 * 64 + 64) * sizeof(float);
+  lds += (size_t)wgemm_red_floats(WAVES, KSPLIT, NG, mt, a.M, a.K) * sizeof(float);
   if (ASRC == A_ATTN)  // chunk factors (fallback path) or chunk-group partials (early path)
     lds += std::max((size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit, (size_t)WAVES * 64 * 8) * sizeof(float);
+  if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
+  const dim3 g(grid, a.sliced ? a.kc : 1);
   if (mt == 1)
-    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY>), dim3(grid),
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY>), g,
+                       dim3(WAVES * 64), lds, s, a);
+  else if (mt == 2)
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 2, NG, KSPLIT, ASRC, NORM, EPI, R, false>), g,
                        dim3(WAVES * 64), lds, s, a);
   else
-    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 4, NG, KSPLIT, ASRC, NORM, EPI, R, false>), dim3(grid),
+    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 4, NG, KSPLIT, ASRC, NORM, EPI, R, false>), g,
                        dim3(WAVES * 64), lds, s, a);
 }
 
@@ -583,7 +666,7 @@ static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
 template <int C, int NG, int ASRC, bool NORM, int EPI>
 static void launch_shape(const WgemmArgs& a, int grid, hipStream_t s) {
   constexpr Shape3 h = kShapes[C];
-  const int S = (a.K / 32) / (h.ksplit * h.ku);
+  const int S = (a.K / 32) / (h.ksplit * h.ku);  // (sliced: stages of one chunk)
   if (h.r >= 2 && S % 2 == 0) launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 2>(a, grid, s);
   else launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 1>(a, grid, s);
 }

@@ -16,17 +16,22 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 // per wave group of every workgroup).  Tiles are stored round-major, then STAGE-major:
 // at stage s every wave of the launch reads one contiguous block (ur*ksplit*NG*ku KiB),
 // the access pattern that streams HBM fastest (scripts/hbm_floor.hip, pipe sweep).
+// K is cut into kc chunks of KT/kc k-tiles (chunk-major): a wave's K part is split evenly
+// over the chunks, so a launch may also run one chunk per workgroup (grid.y = chunk,
+// "K-sliced": the A operand of one chunk fits LDS at batch 17..32; fp32 partials combined
+// by a second kernel).
 struct StreamPlan {
-  int ng = 1, ksplit = 1, ku = 8, waves = 4, grid = 1;
+  int ng = 1, ksplit = 1, ku = 8, waves = 4, grid = 1, kc = 1;
   __host__ __device__ int ur() const { return grid * (waves / ksplit); }
 };
 // Tile index (1 KiB units) of n-tile nt (unit nt/ng, member nt%ng), k-tile kt.
 __host__ __device__ inline long long plan_tile(int ng, int ksplit, int ku, int ur, int units, int KT,
-                                               int nt, int kt) {
+                                               int kc, int nt, int kt) {
   const int u = nt / ng, g = nt - u * ng;
-  const int kt_per = KT / ksplit;
-  const int kp = kt / kt_per, ki = kt - kp * kt_per;
-  const int st = ki / ku, kk = ki - st * ku;
+  const int KTc = KT / kc, kt_pc = KTc / ksplit;
+  const int c = kt / KTc, rr = kt - c * KTc;
+  const int kp = rr / kt_pc, ki = rr - kp * kt_pc;
+  const int st = c * (kt_pc / ku) + ki / ku, kk = ki % ku;
   const int r = u / ur, ui = u - r * ur;
   const int nr = (units - r * ur) < ur ? (units - r * ur) : ur;
   return (long long)r * ur * KT * ng +
@@ -60,6 +65,9 @@ struct WgemmArgs {
   const int* attn_pos = nullptr;
   int attn_split = 0, attn_nsplit = 0, attn_D = 0;
   int ur = 0;         // layout: units per round (StreamPlan::ur, filled in by launch_wgemm)
+  int kc = 1;         // layout: K chunks (StreamPlan::kc, filled in by launch_wgemm)
+  int sliced = 0;     // 1: grid.y = K chunk, K = one chunk, ldx = full K (filled in by launch_wgemm)
+  float* part_out = nullptr;  // K-sliced launches: fp32 partials [kc][M][ldo] (caller's workspace)
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
 };
 
@@ -68,6 +76,7 @@ struct WgemmPlan {
   int cfg = 0;    // kernel instantiation of that shape (lm_gemm.hip)
   int grid = 1;
   bool a_lds = true;
+  bool sliced = false;  // one K chunk per workgroup (grid.y = sp.kc) + combine kernel
 };
 
 // Row-major W [N][K] -> tiles of the matrix's stream plan.  The destination matrix has
@@ -76,8 +85,29 @@ struct WgemmPlan {
 void launch_retile(const bf16_t* w, bf16_t* t, int N, int K, int N_total, int ng, int num_cu,
                    hipStream_t s, int nt_mult = 1, int nt_off = 0);
 WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu);
+// LDS bytes of a wgemm launch whose A operand (M rows x Kl columns) is staged in LDS
+size_t wgemm_lds_bytes(int waves, int ksplit, int ng, int M, int Kl, bool a_in_lds);
+// fp32 partial workspace a K-sliced launch of this plan needs (elements)
+inline size_t wgemm_part_elems(const WgemmPlan& p, int M, int ldo) {
+  return p.sliced ? (size_t)p.sp.kc * M * ldo : 0;
+}
 bool wgemm_supported(int M, int N, int K, int epi);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
+
+// ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
+// MFMA blocks; epilogues EPI_STORE / EPI_RESID / EPI_SWIGLU; no fused RMSNorm
+struct PgemmArgs {
+  const bf16_t* x = nullptr;  // [M][ldx]
+  int M = 0, K = 0, ldx = 0;
+  const bf16_t* w = nullptr;  // tiled weights (the matrix's stream plan, filled in by launch_pgemm)
+  int N = 0;
+  int ng = 1, ksplit = 1, ku = 1, ur = 1, units = 1, kc = 1;
+  bf16_t* out = nullptr;  // [M][ldo]
+  int ldo = 0;
+  bf16_t* resid = nullptr;  // EPI_RESID: updated in place
+};
+bool pgemm_supported(int M, int N, int K, int epi);
+void launch_pgemm(const PgemmArgs& a, int epi, int num_cu, hipStream_t s);
 
 // ---- elementwise / small kernels (lm_ops.hip)
 void launch_rmsnorm(const bf16_t* x, int ldx, const bf16_t* w, float eps, bf16_t* y, int ldy,
@@ -89,6 +119,9 @@ void launch_gather_rows(const bf16_t* x, int ld, const int* rows, bf16_t* y, int
 void launch_synth_fill(void* dst, int dtype, long long n, unsigned long long seed, float scale,
                        hipStream_t s);
 void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s);
+// K-sliced GEMM combine: v = bf16(sum_c part[c][m][n]);  resid ? resid += v : out = v
+void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
+                           bf16_t* resid, int ldo, hipStream_t s);
 
 // ---- attention (lm_attn.hip)
 struct AttnArgs {

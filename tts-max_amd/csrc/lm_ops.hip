@@ -9,19 +9,19 @@ namespace tts {
 // LlamaRMSNorm (transformers modeling_llama.py:62-67) with bf16 in/out.
 __global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, int ldx, const bf16_t* __restrict__ w,
                                float eps, bf16_t* __restrict__ y, int ldy, int K) {
-  __shared__ float red[16];
+  __shared__ float segs[64];  // 512-value segment sums (K <= 32768)
   const bf16_t* xr = x + (size_t)blockIdx.x * ldx;
   bf16_t* yr = y + (size_t)blockIdx.x * ldy;
-  float ss = 0.f;
-  for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
-    const u32x4_t v = *(const u32x4_t*)(xr + k);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float lo = bf_lo(v[q]), hi = bf_hi(v[q]);
-      ss += lo * lo + hi * hi;
-    }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int nseg = (K + 511) / 512;
+  for (int sg = wave; sg < nseg; sg += nw) {  // canonical order (chunk_sumsq)
+    const int k = sg * 512 + lane * 8;
+    const float s = wave_sum_dpp(k < K ? chunk_sumsq(*(const u32x4_t*)(xr + k)) : 0.f);
+    if (lane == 0) segs[sg] = s;
   }
-  ss = block_sum(ss, red);
+  __syncthreads();
+  float ss = 0.f;
+  for (int sg = 0; sg < nseg; ++sg) ss += segs[sg];
   const float r = 1.0f / sqrtf(ss / (float)K + eps);
   for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
     u32x4_t v = *(const u32x4_t*)(xr + k);
@@ -158,6 +158,48 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restri
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x)
     y[i] = f2bf(x[i]);
+}
+
+// K-sliced GEMM epilogue: the chunk partials of one output element summed in chunk order,
+// rounded once to bf16 (as nn.Linear), then stored or added to the residual stream (rounded
+// again, modeling_llama.py decoder residual).  8 columns per thread.
+__global__ void splitk_combine_kernel(const float* __restrict__ part, int kc, int M, int N, int ldp,
+                                      bf16_t* __restrict__ out, bf16_t* __restrict__ resid, int ldo) {
+  const int per_row = N / 8;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * per_row) return;
+  const int m = i / per_row, n = (i - m * per_row) * 8;
+  float v[8];
+  {
+    const float4* p = (const float4*)(part + (size_t)m * ldp + n);
+    const float4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  for (int c = 1; c < kc; ++c) {
+    const float4* p = (const float4*)(part + ((size_t)c * M + m) * ldp + n);
+    const float4 a = p[0], b = p[1];
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
+  u32x4_t pk;
+  if (resid) {
+    bf16_t* r = resid + (size_t)m * ldo + n;
+    const u32x4_t old = *(const u32x4_t*)r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      pk[q] = pack_bf2(bf_lo(old[q]) + rbf(v[2 * q]), bf_hi(old[q]) + rbf(v[2 * q + 1]));
+    *(u32x4_t*)r = pk;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(v[2 * q], v[2 * q + 1]);
+    *(u32x4_t*)(out + (size_t)m * ldo + n) = pk;
+  }
+}
+
+void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
+                           bf16_t* resid, int ldo, hipStream_t s) {
+  const int n = M * (N / 8);
+  hipLaunchKernelGGL(splitk_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, kc, M, N, ldp,
+                     out, resid, ldo);
 }
 
 void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s) {

@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "tts_synth_fill",
     "tts_op_retile",
     "tts_op_wgemm",
+    "tts_op_pgemm",
     "tts_op_rmsnorm",
     "tts_op_gemm_f32",
 )
@@ -152,6 +153,7 @@ def load_library() -> ctypes.CDLL:
         "tts_synth_fill": (I32, [P, I32, I64, U64, F32, P]),
         "tts_op_retile": (I32, [P, P, I32, I32, I32, P]),
         "tts_op_wgemm": (I32, [P, I32, I32, I32, P, I32, P, F32, P, I32, P, I32, P]),
+        "tts_op_pgemm": (I32, [P, I32, I32, P, I32, P, I32, P, I32, P]),
         "tts_op_rmsnorm": (I32, [P, P, F32, P, I32, I32, P]),
         "tts_op_gemm_f32": (I32, [P, I32, I32, I32, P, I32, P, P, I32, P, I32, P]),
     }
