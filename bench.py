@@ -36,6 +36,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MODEL_NAMES = {"tts1": "TTS-1 (Llama-3.2-1B dims, V=193856, tied)",
+               "tts1-max": "TTS-1-Max (Llama-3.1-8B dims, V=193856, untied)"}
 
 
 def log(*a):
@@ -200,7 +202,7 @@ def main():
             "config": {
                 "workload": f"{arch.name} bf16 bs={B}/GPU: prompt {P} tokens ({args.prompt_codes} codes), "
                             f"{N} greedy codes, codec {carch.name} on {codes_per_utt} codes",
-                "model": "TTS-1 (Llama-3.2-1B dims, V=193856, tied) + xcodec2-style codec 24 kHz",
+                "model": MODEL_NAMES.get(arch.name, arch.name) + f" + xcodec2-style codec {carch.name}",
                 "global_batch": B * world,
                 "seq_len": P + N,
                 "parallelism": f"dp{world}",

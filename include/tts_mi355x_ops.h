@@ -39,6 +39,18 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
 tts_status tts_op_pgemm(const void* x, int32_t M, int32_t K, const void* w_tiled, int32_t N, void* out,
                         int32_t ldo, void* resid, int32_t epi, void* stream);
 
+/* Sampling head (GenerationMixin._sample with TemperatureLogitsWarper, TopKLogitsWarper,
+ * TopPLogitsWarper; transformers logits_process.py:238,473,542): rows of processed fp32
+ * logits [B][V] -> one drawn token per row (tokens, device int32 [B]) and, when `probs` is
+ * not NULL, the final distribution written into probs [B][V] at the kept ids (the caller
+ * zero-fills it).  part_max (optional, [B][nparts]) = maxima of disjoint column blocks of
+ * each row, used as the top-k lower bound the engine gets from its lm_head workgroups.
+ * The draw is u = splitmix64(seed, row, step) in [0,1) walked over the kept ids in
+ * descending-probability order (distribution-exact; not torch's RNG stream). */
+tts_status tts_op_sample(const float* logits, int32_t B, int32_t V, float temperature, int32_t top_k,
+                         float top_p, uint64_t seed, int32_t step, const float* part_max, int32_t nparts,
+                         float* probs, int32_t* tokens, void* stream);
+
 /* LlamaRMSNorm over rows of x (bf16). */
 tts_status tts_op_rmsnorm(const void* x, const void* w, float eps, void* y, int32_t M, int32_t K,
                           void* stream);

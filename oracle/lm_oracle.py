@@ -154,3 +154,32 @@ class LlamaOracle:
                 break
             x = self.forward([tok], len(seq) - 1, cache)
         return new, margins
+
+
+def sample_probs(scores: torch.Tensor, temperature: float, top_k: int, top_p: float) -> torch.Tensor:
+    """The distribution GenerationMixin._sample draws from (generation/utils.py:2918-2923,
+    `probs = softmax(next_token_scores)`) after the sampling warpers, in the order
+    _get_logits_processor appends them (generation/utils.py, `if generation_config.do_sample`):
+
+    * TemperatureLogitsWarper (logits_process.py:238-300): scores / T, only when T != 1.0
+    * TopKLogitsWarper (logits_process.py:542-580): k = min(top_k, V); remove
+      `scores < topk(scores, k).values[..., -1]` (ties with the k-th value are kept)
+    * TopPLogitsWarper (logits_process.py:473-540), only when top_p < 1.0: ascending sort,
+      softmax, cumsum; remove `cum <= 1 - top_p`, except the largest (min_tokens_to_keep=1)
+
+    `scores` is one row of processed fp32 logits (after repetition penalty / EOS mask).
+    Pinned against transformers' own warper classes in tests/test_oracle_golden.py."""
+    s = scores.float().clone()
+    if temperature != 1.0:
+        s = s / temperature
+    if top_k and top_k > 0:
+        k = min(top_k, s.numel())
+        kth = torch.topk(s, k).values[-1]
+        s = s.masked_fill(s < kth, float("-inf"))
+    if top_p < 1.0:
+        sv, si = torch.sort(s, descending=False)
+        cum = sv.softmax(dim=-1).cumsum(dim=-1)
+        rm = cum <= (1 - top_p)
+        rm[-1:] = False
+        s = s.masked_fill(rm.scatter(0, si, rm), float("-inf"))
+    return torch.softmax(s, dim=-1)

@@ -103,3 +103,28 @@ def test_synth_generator_known_values():
     assert np.array_equal(v, v2)
     assert np.all(np.abs(v) <= 1.0)
     assert synth.tensor_seed(0x5EED, "a") != synth.tensor_seed(0x5EED, "b")
+
+
+@pytest.mark.parametrize("T,k,p", [(0.8, 50, 1.0), (1.0, 50, 1.0), (0.7, 20, 0.9), (1.3, 5, 0.5), (0.8, 1, 1.0)])
+def test_sample_probs_match_transformers_warpers(T, k, p):
+    """The oracle's sampling distribution == transformers' warpers + softmax (the reference's
+    dependency, installed here), on rows with ties, -inf (masked EOS) and a peaked head."""
+    from transformers.generation.logits_process import (LogitsProcessorList, TemperatureLogitsWarper,
+                                                        TopKLogitsWarper, TopPLogitsWarper)
+
+    g = torch.Generator().manual_seed(int(T * 100) + k)
+    for trial in range(4):
+        s = torch.randn(1, 3000, generator=g) * 3
+        s = s.to(torch.bfloat16).float()  # bf16-rounded logits: many exact ties
+        s[0, 17] = float("-inf")
+        if trial == 1:
+            s[0, :40] = 9.0  # a tie block straddling k
+        warpers = LogitsProcessorList()
+        if T != 1.0:
+            warpers.append(TemperatureLogitsWarper(T))
+        warpers.append(TopKLogitsWarper(k))
+        if p < 1.0:
+            warpers.append(TopPLogitsWarper(p))
+        ref = torch.softmax(warpers(None, s.clone()), dim=-1)[0]
+        got = lm_oracle.sample_probs(s[0], T, k, p)
+        assert torch.allclose(got, ref, atol=1e-7, rtol=0), (got - ref).abs().max()

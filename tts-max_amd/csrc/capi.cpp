@@ -245,6 +245,23 @@ tts_status tts_op_pgemm(const void* x, int32_t M, int32_t K, const void* w_tiled
   });
 }
 
+tts_status tts_op_sample(const float* logits, int32_t B, int32_t V, float temperature, int32_t top_k,
+                         float top_p, uint64_t seed, int32_t step, const float* part_max, int32_t nparts,
+                         float* probs, int32_t* tokens, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(logits && tokens && B >= 1 && V >= 1, "bad arguments");
+    TTS_REQUIRE(temperature > 0.f && top_k >= 1 && top_k <= SAMPLE_MAX_TOP_K && top_p > 0.f && top_p <= 1.f,
+                "temperature > 0, top_k in [1, 1024], top_p in (0, 1]");
+    SampleArgs a;
+    a.logits = logits; a.ldl = V; a.V = V;
+    a.temperature = temperature; a.top_k = top_k; a.top_p = top_p; a.seed = seed; a.step0 = step;
+    a.part_val = part_max; a.nparts = part_max ? nparts : 0; a.part_stride = nparts;
+    a.probs = probs; a.tokens = tokens;
+    launch_sample(a, B, (hipStream_t)stream);
+    HIP_CHECK(hipGetLastError());
+  });
+}
+
 tts_status tts_op_rmsnorm(const void* x, const void* w, float eps, void* y, int32_t M, int32_t K,
                           void* stream) {
   return guarded([&] {

@@ -85,6 +85,7 @@ struct LmWork {
   DevBuf part_o, part_ml;                           // attention split partials
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
+  DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
   DevBuf logits;                                    // scoring output (bf16)
   DevBuf row_slot, row_pos, row_idx;                // prefill row descriptors
   DevBuf st_int;                                    // step-state ints
@@ -97,6 +98,10 @@ struct LmWork {
   int graph_batch = -1;  // the captured step bakes in B, penalty, eos and min_new
   float graph_pen = -1.f;
   int graph_eos = -2, graph_min_new = -1;
+  // sampling parameters baked into the captured step (kernel arguments)
+  int graph_sample = -1, graph_top_k = -1;
+  float graph_temp = -1.f, graph_top_p = -1.f;
+  unsigned long long graph_seed = 0;
   int* h_active = nullptr;  // pinned host copy of n_active (ring of 2)
 };
 

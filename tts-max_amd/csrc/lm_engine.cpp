@@ -248,6 +248,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
     const int kmax = std::max(HID, std::max(FF, H * D));
     w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
   }
+  w.slogits.alloc((size_t)B * V * 4);
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.row_slot.alloc((size_t)R * 4);
@@ -402,18 +403,31 @@ struct Ctx {
     return st;
   }
 
-  // lm_head over B rows of `xin` + greedy finalize (state update, next embedding -> w.x)
-  void head_and_pick(const bf16_t* xin, int B, const StepState& st, float penalty) {
+  // lm_head over B rows of `xin` + the pick (greedy argmax, or the sampling head) + finalize
+  // (state update, next embedding -> w.x)
+  void head_and_pick(const bf16_t* xin, int B, const StepState& st, const tts_gen_params& gp) {
     WgemmArgs ex;
-    ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = penalty;
+    ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = gp.repetition_penalty;
     ex.eos_mask = st.eos_mask;
     ex.part_val = w.lpart_v.as<float>(); ex.part_idx = w.lpart_i.as<int>();
     ex.part_stride = LOGITS_MAX_PARTS;
+    if (gp.do_sample) { ex.logits_out = w.slogits.as<float>(); ex.ldl = c.vocab_size; }
     TTS_REQUIRE(B <= kPrefillChunk, "batch larger than one GEMM chunk");
     WgemmPlan p = plan_wgemm(B, c.vocab_size, c.hidden_size, EPI_LOGITS, e->num_cu);
     gemm(xin, B, c.hidden_size, M.lm_head, c.vocab_size, M.final_norm, nullptr, 0, nullptr,
          EPI_LOGITS, &ex);
-    launch_finalize_greedy(ex.part_val, ex.part_idx, LOGITS_MAX_PARTS, p.grid, st, B,
+    int nparts = p.grid;
+    if (gp.do_sample) {
+      SampleArgs sa;
+      sa.logits = w.slogits.as<float>(); sa.ldl = c.vocab_size; sa.V = c.vocab_size;
+      sa.temperature = gp.temperature; sa.top_k = gp.top_k; sa.top_p = gp.top_p;
+      sa.seed = gp.seed; sa.step = st.gen_count; sa.done = st.done;
+      sa.part_val = ex.part_val; sa.nparts = p.grid; sa.part_stride = LOGITS_MAX_PARTS;
+      sa.out_part_val = ex.part_val; sa.out_part_idx = ex.part_idx;
+      launch_sample(sa, B, s);
+      nparts = 1;
+    }
+    launch_finalize_greedy(ex.part_val, ex.part_idx, LOGITS_MAX_PARTS, nparts, st, B,
                            M.embed_rows.as<bf16_t>(), w.x.as<bf16_t>(), c.hidden_size, s);
   }
 };
@@ -450,7 +464,12 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(p != nullptr && ids != nullptr && lens != nullptr, "null argument");
   TTS_REQUIRE(B >= 1 && B <= e->w.cap_batch, "batch out of range");
-  TTS_REQUIRE(!p->do_sample, "sampling (do_sample=1) is not implemented yet; use greedy");
+  if (p->do_sample) {  // HF: TemperatureLogitsWarper requires T > 0; top_k from GenerationConfig (50)
+    TTS_REQUIRE(p->temperature > 0.f, "sampling needs temperature > 0 (temperature 0 = greedy)");
+    TTS_REQUIRE(p->top_k >= 1 && p->top_k <= SAMPLE_MAX_TOP_K,
+                "sampling supports top_k in [1, 1024] (HF default 50; full-vocabulary sampling is not built)");
+    TTS_REQUIRE(p->top_p > 0.f && p->top_p <= 1.f, "top_p must be in (0, 1]");
+  }
   Ctx X(e, s);
   const tts_lm_config& c = X.c;
   const int V = c.vocab_size;
@@ -494,7 +513,7 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
   HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, last_rows.data(), B * 4, hipMemcpyHostToDevice, s));
   launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, e->w.row_idx.as<int>(),
                      e->w.last_x.as<bf16_t>(), B, c.hidden_size, s);
-  X.head_and_pick(e->w.last_x.as<bf16_t>(), B, st, p->repetition_penalty);
+  X.head_and_pick(e->w.last_x.as<bf16_t>(), B, st, *p);
   check_launch();
   HIP_CHECK(hipEventRecord(e->ev[3], s));
 
@@ -504,15 +523,21 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
   HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, ident.data(), B * 4, hipMemcpyHostToDevice, s));
   // (the embedding of each sequence's next token is already in w.x rows 0..B-1)
   const float pen = p->repetition_penalty;
+  const tts_gen_params gp = *p;
   auto step = [&](hipStream_t ss) {
     Ctx Y(e, ss);
     Y.layers(B, e->w.row_slot.as<int>(), st.pos, true);
-    Y.head_and_pick(e->w.x.as<bf16_t>(), B, st, pen);
+    Y.head_and_pick(e->w.x.as<bf16_t>(), B, st, gp);
   };
-  // the graph bakes in B, the penalty and eos/min_new (kernel args): recapture on change
+  // the graph bakes in B, the penalty, eos/min_new and the sampling parameters (kernel
+  // args): recapture on change
   LmWork& W = e->w;
+  const bool smp_changed =
+      W.graph_sample != p->do_sample ||
+      (p->do_sample && (W.graph_temp != p->temperature || W.graph_top_k != p->top_k ||
+                        W.graph_top_p != p->top_p || W.graph_seed != p->seed));
   if (W.graph && (W.graph_batch != B || W.graph_pen != pen || W.graph_eos != p->eos_token_id ||
-                  W.graph_min_new != p->min_new_tokens)) {
+                  W.graph_min_new != p->min_new_tokens || smp_changed)) {
     hipGraphExecDestroy(e->w.graph);
     e->w.graph = nullptr;
   }
@@ -530,6 +555,11 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
     W.graph_pen = pen;
     W.graph_eos = p->eos_token_id;
     W.graph_min_new = p->min_new_tokens;
+    W.graph_sample = p->do_sample;
+    W.graph_temp = p->temperature;
+    W.graph_top_k = p->top_k;
+    W.graph_top_p = p->top_p;
+    W.graph_seed = p->seed;
   }
   int steps = 0;
   int polls = 0;

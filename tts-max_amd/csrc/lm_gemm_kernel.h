@@ -562,6 +562,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             const uint32_t bits = seen_cur[mt][r];
             if ((bits >> (n & 31)) & 1u) v = (v < 0.f) ? v * a.penalty : v / a.penalty;
             if (n == eosr[mt][r]) v = -INFINITY;
+            if (a.logits_out) a.logits_out[(size_t)m * a.ldl + n] = v;
             argmax_merge(best_v[mt][r], best_i[mt][r], v, n);
           }
         }

@@ -64,6 +64,8 @@ struct WgemmArgs {
   const float* attn_ml = nullptr;
   const int* attn_pos = nullptr;
   int attn_split = 0, attn_nsplit = 0, attn_D = 0;
+  float* logits_out = nullptr;  // EPI_LOGITS: also store the processed fp32 logits [M][ldl] (sampling)
+  int ldl = 0;
   int ur = 0;         // layout: units per round (StreamPlan::ur, filled in by launch_wgemm)
   int kc = 1;         // layout: K chunks (StreamPlan::kc, filled in by launch_wgemm)
   int sliced = 0;     // 1: grid.y = K chunk, K = one chunk, ldx = full K (filled in by launch_wgemm)
@@ -153,6 +155,27 @@ void launch_attn_decode_step(const AttnArgs& a, hipStream_t s);
 // bf16 output in a.out [rows][H*D]
 void launch_attn_decode_merged(const AttnArgs& a, hipStream_t s);
 void launch_attn_combine(const AttnArgs& a, hipStream_t s);
+
+// ---- sampling head (lm_sample.hip): temperature, top-k, top-p, multinomial draw
+struct SampleArgs {
+  const float* logits = nullptr;  // processed logits [B][ldl]
+  int ldl = 0, V = 0;
+  float temperature = 1.f;
+  int top_k = 50;                 // 1 .. 1024
+  float top_p = 1.f;
+  unsigned long long seed = 0;
+  const int* step = nullptr;      // per-row draw counter (generated count), or step0
+  int step0 = 0;
+  const int* done = nullptr;      // rows already stopped (skipped)
+  const float* part_val = nullptr;  // lm_head workgroup maxima [B][part_stride] (top-k bound)
+  int nparts = 0, part_stride = 0;
+  float* out_part_val = nullptr;  // chosen token as the single "partial" finalize reads
+  int* out_part_idx = nullptr;
+  float* probs = nullptr;         // optional: final distribution [B][ldl] (kept ids only)
+  int* tokens = nullptr;          // optional: chosen token [B]
+};
+constexpr int SAMPLE_MAX_TOP_K = 1024;
+void launch_sample(const SampleArgs& a, int B, hipStream_t s);
 
 // ---- sampling / bookkeeping (lm_ops.hip)
 struct StepState {

@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "tts_op_retile",
     "tts_op_wgemm",
     "tts_op_pgemm",
+    "tts_op_sample",
     "tts_op_rmsnorm",
     "tts_op_gemm_f32",
 )
@@ -154,6 +155,7 @@ def load_library() -> ctypes.CDLL:
         "tts_op_retile": (I32, [P, P, I32, I32, I32, P]),
         "tts_op_wgemm": (I32, [P, I32, I32, I32, P, I32, P, F32, P, I32, P, I32, P]),
         "tts_op_pgemm": (I32, [P, I32, I32, P, I32, P, I32, P, I32, P]),
+        "tts_op_sample": (I32, [P, I32, I32, F32, I32, F32, ctypes.c_uint64, I32, P, I32, P, P, P]),
         "tts_op_rmsnorm": (I32, [P, P, F32, P, I32, I32, P]),
         "tts_op_gemm_f32": (I32, [P, I32, I32, I32, P, I32, P, P, I32, P, I32, P]),
     }

@@ -177,11 +177,16 @@ class MI355XSpeechLM:
     def generate_batch(self, prompts: Sequence[Sequence[int]], max_length: int, min_new_tokens: int = 0,
                        eos_token_id: int = -1, do_sample: bool = False, repetition_penalty: float = 1.0,
                        top_p: float = 1.0, temperature: float = 1.0, top_k: int | None = None,
-                       seed: int = 0) -> list[list[int]]:
-        """Independent sequences (each as its batch-1 HF generate): returns new tokens."""
-        if do_sample:
-            raise NotImplementedError("sampling (do_sample=True) is not implemented in round 1; "
-                                      "use temperature=0 (greedy)")
+                       seed: int | None = None) -> list[list[int]]:
+        """Independent sequences (each as its batch-1 HF generate): returns new tokens.
+
+        do_sample: GenerationMixin._sample's warpers (temperature, top_k — HF default 50 —,
+        top_p) and a multinomial draw from the engine's counter-based RNG.  `seed=None`
+        draws the seed from torch's default generator, so torch.manual_seed() makes runs
+        reproducible as it does for HF (the token streams differ from HF's: only the
+        distribution is shared)."""
+        if do_sample and seed is None:
+            seed = int(torch.randint(0, 2**62, (1,)).item())
         B = len(prompts)
         if B < 1 or B > self.max_batch:
             raise ValueError(f"batch {B} outside [1, max_batch={self.max_batch}]")
@@ -194,8 +199,9 @@ class MI355XSpeechLM:
         out = np.zeros((B, stride), dtype=np.int32)
         out_lens = np.zeros(B, dtype=np.int32)
         params = _lib.GenParams(max_length=max_length, min_new_tokens=min_new_tokens, eos_token_id=eos_token_id,
-                                do_sample=0, repetition_penalty=repetition_penalty, temperature=temperature,
-                                top_p=top_p, top_k=50 if top_k is None else top_k, seed=seed)
+                                do_sample=1 if do_sample else 0, repetition_penalty=repetition_penalty,
+                                temperature=temperature, top_p=top_p, top_k=50 if top_k is None else top_k,
+                                seed=0 if seed is None else seed)
         pi32 = ctypes.POINTER(ctypes.c_int32)
         _lib.check(self._lib.tts_generate(self._h, ctypes.byref(params), flat.ctypes.data_as(pi32),
                                           lens.ctypes.data_as(pi32), B, out.ctypes.data_as(pi32), stride,
@@ -204,16 +210,23 @@ class MI355XSpeechLM:
 
     def _generate_vllm_form(self, prompt_token_ids, sampling_params):
         sp = sampling_params
-        temperature = getattr(sp, "temperature", 0.0)
-        if temperature and temperature > 0:
-            raise NotImplementedError("sampling is not implemented in round 1; use temperature=0")
+        temperature = float(getattr(sp, "temperature", 1.0) or 0.0)
+        if temperature > 0 and float(getattr(sp, "frequency_penalty", 0.0) or 0.0) != 0.0:
+            raise NotImplementedError("vLLM frequency_penalty is not implemented (HF-form sampling is)")
+        top_k = int(getattr(sp, "top_k", -1) or -1)
+        if temperature > 0 and top_k <= 0:
+            raise NotImplementedError("full-vocabulary sampling (vLLM top_k=-1) is not built; pass top_k")
         max_tokens = int(getattr(sp, "max_tokens", 16))
         stop = list(getattr(sp, "stop_token_ids", None) or [])
         prompt = list(prompt_token_ids)
         new = self.generate_batch([prompt], max_length=len(prompt) + max_tokens,
                                   min_new_tokens=int(getattr(sp, "min_tokens", 0)),
                                   eos_token_id=stop[0] if stop else -1,
-                                  repetition_penalty=float(getattr(sp, "repetition_penalty", 1.0)))[0]
+                                  repetition_penalty=float(getattr(sp, "repetition_penalty", 1.0)),
+                                  do_sample=temperature > 0, temperature=temperature or 1.0,
+                                  top_p=float(getattr(sp, "top_p", 1.0)),
+                                  top_k=top_k if top_k > 0 else None,
+                                  seed=getattr(sp, "seed", None))[0]
         return [RequestOutput(prompt_token_ids=prompt, outputs=[CompletionOutput(token_ids=new)])]
 
     # ------------------------------------------------------------------ utilities ------
