@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--kernel-iters", type=int, default=30)
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the N=1 secondary lines (bs=32 batched decode, bs=8 streaming latency)")
     args = ap.parse_args()
 
     from tts_amd import configs, synth
@@ -95,16 +97,21 @@ def main():
 
     max_seq = P + N + 16
     t0 = time.time()
-    lm = MI355XSpeechLM.synthetic(arch, seed=0x5EED, device=local, max_batch=B, max_seq_len=max_seq)
+    secondary = (world == 1 and not args.no_secondary)
+    lm = MI355XSpeechLM.synthetic(arch, seed=0x5EED, device=local, max_batch=max(B, 32 if secondary else 1),
+                                  max_seq_len=max_seq)
     dec = MI355XAudioDecoder.synthetic(carch, seed=0xC0DEC, device=local, max_codes=args.prompt_codes + N + 8)
     log(f"[rank {rank}] engine ready in {time.time() - t0:.1f}s")
     codes_per_utt = args.prompt_codes + N
 
-    def one_step():
-        if dist is not None:
-            dist.broadcast(req, src=0)
-        mine = req[rank * B:(rank + 1) * B].cpu()
-        prompts = [mine[i, 1:1 + int(mine[i, 0])].tolist() for i in range(B)]
+    def one_step(B=B, local_prompts=None):
+        if local_prompts is not None:
+            prompts = local_prompts
+        else:
+            if dist is not None:
+                dist.broadcast(req, src=0)
+            mine = req[rank * B:(rank + 1) * B].cpu()
+            prompts = [mine[i, 1:1 + int(mine[i, 0])].tolist() for i in range(B)]
         new = lm.generate_batch(prompts, max_length=P + N, min_new_tokens=N, eos_token_id=vocab.speech_end_id,
                                 repetition_penalty=1.1)
         # codec input = prompt speech codes + generated codes (ids -> codes via the LUT)
@@ -113,6 +120,8 @@ def main():
             codes = [c for c in lm.ids_to_codes(p[-args.prompt_codes:] + n) if c >= 0]
             utts.append(codes)
         wav = dec.decode_batch(utts, out=wav_buf)
+        if local_prompts is not None:
+            return sum(len(n) for n in new), wav
         out = torch.full((B, N), -1, dtype=torch.int32, device=dev)
         for i, n in enumerate(new):
             out[i, :len(n)] = torch.tensor(n, dtype=torch.int32)
@@ -121,7 +130,8 @@ def main():
             dist.gather(out, gathered, dst=0)
         return sum(len(n) for n in new), wav
 
-    wav_buf = torch.empty(B * codes_per_utt * carch.samples_per_code, dtype=torch.float32, device=dev)
+    wav_buf = torch.empty(max(B, 32 if secondary else 1) * codes_per_utt * carch.samples_per_code,
+                          dtype=torch.float32, device=dev)
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
@@ -177,6 +187,44 @@ def main():
                                      frac=round(step_bytes / step_ms / 1e6 / HBM_PEAK_GBS, 4)),
                     kernels={k: dict(avg_ms=round(v["avg_ms"], 5), gbs=round(v["gbs"], 1)) for k, v in kern.items()})
 
+    sec = None
+    if secondary:
+        sec = {}
+        # configs[2]: bs=32 batched greedy decode (+ codec), same prompt shape
+        p32 = [synth.synthetic_prompt(vocab, 1000 + u, args.text_tokens, args.prompt_codes) for u in range(32)]
+        one_step(32, p32)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        reps = max(1, min(args.steps, 2))
+        n32 = sum(one_step(32, p32)[0] for _ in range(reps))
+        torch.cuda.synchronize()
+        e32 = (time.perf_counter() - t) / reps
+        a32, b32, k32 = lm.last_timing()
+        sec["bs32"] = dict(value=round(n32 / reps / e32, 2), unit="audio-codes/s", ms_per_step=round(1000 * e32, 3),
+                           x_realtime=round(32 * N / carch.token_rate / e32, 2), lm_prefill_ms=round(a32, 3),
+                           lm_decode_ms=round(b32, 3), decode_step_ms=round(b32 / max(k32, 1), 4))
+        # configs[4]: streaming, bs=8, chunks of 25 codes voiced with 25 codes of left context
+        from tts_amd.streaming import StreamingSynthesizer
+
+        p8 = p32[:8]
+        pc8 = [[c for c in lm.ids_to_codes(p[-args.prompt_codes:]) if c >= 0] for p in p8]
+        ss = StreamingSynthesizer(lm, dec, chunk=25, left_context=25)
+        firsts, totals = [], []
+        for r in range(3):
+            first = None
+            t = time.perf_counter()
+            for out, el in ss.stream(p8, pc8, max_length=P + N, min_new_tokens=N,
+                                     eos_token_id=vocab.speech_end_id, repetition_penalty=1.1):
+                if first is None:
+                    first = el
+            if r > 0:  # first run warms the graph for batch 8
+                firsts.append(first)
+                totals.append(time.perf_counter() - t)
+        sec["stream_bs8"] = dict(p50_first_audio_ms=round(1000 * float(np.median(firsts)), 3),
+                                 chunk_codes=25, left_context_codes=25,
+                                 codes_per_s=round(8 * N / float(np.median(totals)), 2))
+        log(f"secondary: {sec}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(arch, carch, prompts_all[0], N, args)
@@ -194,7 +242,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random-init TTS-1 weights, synthetic prompt ids of the reference prompt shape)",
+            "data": f"synthetic (random-init {arch.name} weights, synthetic prompt ids of the reference prompt shape)",
             "rtf": round(rtf, 5),
             "x_realtime": round(1.0 / rtf * B, 2),
             "lm_prefill_ms": round(lm_prefill / args.steps, 3),
@@ -209,6 +257,7 @@ def main():
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "secondary": sec,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -128,6 +128,19 @@ tts_status tts_generate(tts_engine* e, const tts_gen_params* p, const int32_t* p
                         const int32_t* prompt_lens, int32_t batch, int32_t* out_ids,
                         int32_t out_stride, int32_t* out_lens, void* stream);
 
+/* The same generation in pieces, for streaming callers (config 5: chunked AR decode with an
+ * incremental codec).  tts_generate_begin validates, prefills and picks the first new
+ * token of every sequence; tts_generate_continue runs up to `n_steps` further decode
+ * steps (*all_done = 1 once every sequence has stopped: EOS or max_length);
+ * tts_generate_read copies the new tokens produced so far (same layout as tts_generate's
+ * outputs) and may be called after every continue.  Tokens are identical to one
+ * tts_generate call with the same arguments.  One open generation per engine; a new
+ * begin (or tts_generate) discards it. */
+tts_status tts_generate_begin(tts_engine* e, const tts_gen_params* p, const int32_t* prompt_ids,
+                              const int32_t* prompt_lens, int32_t batch, void* stream);
+tts_status tts_generate_continue(tts_engine* e, int32_t n_steps, int32_t* all_done);
+tts_status tts_generate_read(tts_engine* e, int32_t* out_ids, int32_t out_stride, int32_t* out_lens);
+
 /* Teacher-forced scoring (parity / debugging): runs the prefill over full sequences and
  * writes the bf16-rounded logits of the last `n_last` positions of each sequence, as
  * fp32, to host `logits` [batch][n_last][vocab]. */

@@ -100,6 +100,34 @@ tts_status tts_generate(tts_engine* e, const tts_gen_params* p, const int32_t* p
   });
 }
 
+tts_status tts_generate_begin(tts_engine* e, const tts_gen_params* p, const int32_t* prompt_ids,
+                              const int32_t* prompt_lens, int32_t batch, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(e && p && prompt_ids && prompt_lens, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_gen_begin(E, p, prompt_ids, prompt_lens, batch, pick_stream(E, stream));
+  });
+}
+
+tts_status tts_generate_continue(tts_engine* e, int32_t n_steps, int32_t* all_done) {
+  return guarded([&] {
+    TTS_REQUIRE(e && all_done && n_steps >= 0, "bad argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    *all_done = lm_gen_continue(E, n_steps);
+  });
+}
+
+tts_status tts_generate_read(tts_engine* e, int32_t* out_ids, int32_t out_stride, int32_t* out_lens) {
+  return guarded([&] {
+    TTS_REQUIRE(e && out_ids && out_lens, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_gen_read(E, out_ids, out_stride, out_lens);
+  });
+}
+
 tts_status tts_lm_score(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
                         int32_t n_last, float* logits, void* stream) {
   return guarded([&] {

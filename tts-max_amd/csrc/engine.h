@@ -117,6 +117,13 @@ struct Engine {
   Codec* codec = nullptr;
   float t_prefill_ms = 0.f, t_decode_ms = 0.f;
   int decode_steps = 0;
+  // an open generation (tts_generate_begin .. tts_generate_read): state lives on the device
+  struct Gen {
+    bool open = false;
+    int B = 0, max_new = 0, launched = 0, polls = 0;
+    bool finished = false;
+    hipStream_t s = nullptr;
+  } gen;
   ~Engine();
 };
 
@@ -124,6 +131,12 @@ hipStream_t pick_stream(Engine* e, void* s);
 void lm_load(Engine* e, const tts_lm_config* cfg, const tts_tensor_desc* t, int n);
 void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens,
                  int B, int32_t* out_ids, int out_stride, int32_t* out_lens, hipStream_t s);
+// the same loop in pieces (streaming): begin = prefill + first token; continue = up to
+// n_steps more decode steps (returns 1 when every row has stopped); read = ids so far
+void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens, int B,
+                  hipStream_t s);
+int lm_gen_continue(Engine* e, int n_steps);
+void lm_gen_read(Engine* e, int32_t* out_ids, int out_stride, int32_t* out_lens);
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
               float* logits, hipStream_t s);
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,

@@ -459,8 +459,8 @@ static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, 
                X.c.hidden_size, X.s);
 }
 
-void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens,
-                 int B, int32_t* out_ids, int out_stride, int32_t* out_lens, hipStream_t s) {
+void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens, int B,
+                  hipStream_t s) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(p != nullptr && ids != nullptr && lens != nullptr, "null argument");
   TTS_REQUIRE(B >= 1 && B <= e->w.cap_batch, "batch out of range");
@@ -485,7 +485,7 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
     TTS_REQUIRE(P < p->max_length, "input length >= max_length");
     const int limit = p->max_length - P;
     TTS_REQUIRE(P + limit <= c.max_seq_len, "prompt + max new tokens exceed max_seq_len");
-    TTS_REQUIRE(limit <= out_stride && limit <= e->w.out_cap, "out_stride too small");
+    TTS_REQUIRE(limit <= e->w.out_cap, "max new tokens exceed the output capacity");
     for (int i = 0; i < P; ++i) {
       const int t = ids[off + i];
       TTS_REQUIRE(t >= 0 && t < V, "token id out of range");
@@ -561,38 +561,83 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
     W.graph_top_p = p->top_p;
     W.graph_seed = p->seed;
   }
-  int steps = 0;
-  int polls = 0;
-  for (int k = 1; k < max_new; ++k) {
+  Engine::Gen& G = e->gen;
+  G.open = true;
+  G.B = B;
+  G.max_new = max_new;
+  G.launched = 1;  // the prefill's head produced the first token
+  G.polls = 0;
+  G.finished = max_new <= 1;
+  G.s = s;
+  e->decode_steps = 0;
+}
+
+// Up to n_steps decode-step graph replays.  The host polls the device's active-row counter
+// every kPollEvery steps, one poll behind (no per-step D->H sync; HF syncs every step,
+// generation/utils.py:2936-2937): a stopped row runs idle (its kernels skip it) until the
+// poll sees every row done.
+int lm_gen_continue(Engine* e, int n_steps) {
+  Engine::Gen& G = e->gen;
+  TTS_REQUIRE(G.open, "no generation in progress (tts_generate_begin)");
+  const hipStream_t s = G.s;
+  const StepState st = Ctx(e, s).state(G.B, e->w.graph_eos, e->w.graph_min_new);
+  for (int n = 0; n < n_steps && !G.finished; ++n) {
+    if (G.launched >= G.max_new) { G.finished = true; break; }
     HIP_CHECK(hipGraphLaunch(e->w.graph, s));
-    ++steps;
-    if (k % kPollEvery == 0) {
-      const int slot = polls & 1;
+    ++G.launched;
+    ++e->decode_steps;
+    if (G.launched % kPollEvery == 0) {
+      const int slot = G.polls & 1;
       HIP_CHECK(hipMemcpyAsync(&e->w.h_active[slot], st.n_active, 4, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipEventRecord(e->ev[slot], s));
-      if (polls > 0) {
+      if (G.polls > 0) {
         HIP_CHECK(hipEventSynchronize(e->ev[slot ^ 1]));
-        if (e->w.h_active[slot ^ 1] == 0) break;
+        if (e->w.h_active[slot ^ 1] == 0) G.finished = true;
       }
-      ++polls;
+      ++G.polls;
     }
   }
-  HIP_CHECK(hipEventRecord(e->ev[1], s));
-  // ---- results
-  std::vector<int> gc(B);
-  HIP_CHECK(hipMemcpyAsync(gc.data(), st.gen_count, B * 4, hipMemcpyDeviceToHost, s));
+  if (G.launched >= G.max_new) G.finished = true;
+  if (!G.finished) {  // exact answer for a streaming caller: sync once per chunk
+    int act = 0;
+    HIP_CHECK(hipMemcpyAsync(&act, st.n_active, 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (act == 0) G.finished = true;
+  }
+  return G.finished ? 1 : 0;
+}
+
+void lm_gen_read(Engine* e, int32_t* out_ids, int out_stride, int32_t* out_lens) {
+  Engine::Gen& G = e->gen;
+  TTS_REQUIRE(G.open, "no generation in progress (tts_generate_begin)");
+  const hipStream_t s = G.s;
+  const StepState st = Ctx(e, s).state(G.B, e->w.graph_eos, e->w.graph_min_new);
+  std::vector<int> gc(G.B);
+  HIP_CHECK(hipMemcpyAsync(gc.data(), st.gen_count, G.B * 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  for (int b = 0; b < B; ++b) {
+  for (int b = 0; b < G.B; ++b) {
+    TTS_REQUIRE(gc[b] <= out_stride, "out_stride too small");
     out_lens[b] = gc[b];
     HIP_CHECK(hipMemcpy(out_ids + (size_t)b * out_stride, st.out_ids + (size_t)b * st.out_stride,
                         (size_t)gc[b] * 4, hipMemcpyDeviceToHost));
   }
+}
+
+void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens,
+                 int B, int32_t* out_ids, int out_stride, int32_t* out_lens, hipStream_t s) {
+  for (int b = 0; b < B; ++b)
+    TTS_REQUIRE(p->max_length - lens[b] <= out_stride, "out_stride too small");
+  lm_gen_begin(e, p, ids, lens, B, s);
+  const int max_new = e->gen.max_new;
+  lm_gen_continue(e, max_new);
+  HIP_CHECK(hipEventRecord(e->ev[1], s));
+  lm_gen_read(e, out_ids, out_stride, out_lens);
   float t0 = 0.f, t1 = 0.f;
   HIP_CHECK(hipEventElapsedTime(&t0, e->ev[2], e->ev[3]));
   HIP_CHECK(hipEventElapsedTime(&t1, e->ev[3], e->ev[1]));
   e->t_prefill_ms = t0;
   e->t_decode_ms = t1;
-  e->decode_steps = steps;
+  e->gen.open = false;
 }
 
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,

@@ -33,6 +33,9 @@ EXPORTED_SYMBOLS = (
     "tts_engine_destroy",
     "tts_lm_load",
     "tts_generate",
+    "tts_generate_begin",
+    "tts_generate_continue",
+    "tts_generate_read",
     "tts_lm_score",
     "tts_lm_id_to_code",
     "tts_lm_last_timing",
@@ -144,6 +147,9 @@ def load_library() -> ctypes.CDLL:
         "tts_engine_destroy": (None, [P]),
         "tts_lm_load": (I32, [P, ctypes.POINTER(LmConfig), ctypes.POINTER(TensorDesc), I32]),
         "tts_generate": (I32, [P, ctypes.POINTER(GenParams), pi32, pi32, I32, pi32, I32, pi32, P]),
+        "tts_generate_begin": (I32, [P, ctypes.POINTER(GenParams), pi32, pi32, I32, P]),
+        "tts_generate_continue": (I32, [P, I32, pi32]),
+        "tts_generate_read": (I32, [P, pi32, I32, pi32]),
         "tts_lm_score": (I32, [P, pi32, pi32, I32, I32, ctypes.POINTER(ctypes.c_float), P]),
         "tts_lm_id_to_code": (I32, [P, pi32, I32, pi32]),
         "tts_lm_last_timing": (I32, [P, ctypes.POINTER(F32), ctypes.POINTER(F32), pi32]),

@@ -208,6 +208,43 @@ class MI355XSpeechLM:
                                           out_lens.ctypes.data_as(pi32), None))
         return [out[b, :out_lens[b]].tolist() for b in range(B)]
 
+    def generate_stream(self, prompts: Sequence[Sequence[int]], max_length: int, chunk: int = 25,
+                        min_new_tokens: int = 0, eos_token_id: int = -1, do_sample: bool = False,
+                        repetition_penalty: float = 1.0, top_p: float = 1.0, temperature: float = 1.0,
+                        top_k: int | None = None, seed: int | None = None):
+        """Chunked generation (config 5): yields (new_tokens_per_row, all_done) after the first
+        token and then after every `chunk` further decode steps.  The rows' final tokens are
+        identical to generate_batch with the same arguments (same device loop, paused)."""
+        if do_sample and seed is None:
+            seed = int(torch.randint(0, 2**62, (1,)).item())
+        B = len(prompts)
+        if B < 1 or B > self.max_batch:
+            raise ValueError(f"batch {B} outside [1, max_batch={self.max_batch}]")
+        lens = np.array([len(p) for p in prompts], dtype=np.int32)
+        if int(lens.max()) >= max_length:
+            raise ValueError(f"Input length of input_ids is {int(lens.max())}, but `max_length` is set to {max_length}.")
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(p, dtype=np.int32) for p in prompts]))
+        params = _lib.GenParams(max_length=max_length, min_new_tokens=min_new_tokens, eos_token_id=eos_token_id,
+                                do_sample=1 if do_sample else 0, repetition_penalty=repetition_penalty,
+                                temperature=temperature, top_p=top_p, top_k=50 if top_k is None else top_k,
+                                seed=0 if seed is None else seed)
+        pi32 = ctypes.POINTER(ctypes.c_int32)
+        _lib.check(self._lib.tts_generate_begin(self._h, ctypes.byref(params), flat.ctypes.data_as(pi32),
+                                                lens.ctypes.data_as(pi32), B, None))
+        stride = max(1, max_length - int(lens.min()))
+        out = np.zeros((B, stride), dtype=np.int32)
+        out_lens = np.zeros(B, dtype=np.int32)
+        done = ctypes.c_int32(0)
+        steps = 0
+        while True:
+            _lib.check(self._lib.tts_generate_read(self._h, out.ctypes.data_as(pi32), stride,
+                                                   out_lens.ctypes.data_as(pi32)))
+            yield [out[b, :out_lens[b]].tolist() for b in range(B)], bool(done.value)
+            if done.value:
+                return
+            _lib.check(self._lib.tts_generate_continue(self._h, chunk, ctypes.byref(done)))
+            steps += 1
+
     def _generate_vllm_form(self, prompt_token_ids, sampling_params):
         sp = sampling_params
         temperature = float(getattr(sp, "temperature", 1.0) or 0.0)
