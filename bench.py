@@ -178,9 +178,19 @@ def main():
     step_ms = lm_decode / max(dec_steps, 1)
     kv_ctx_bytes = B * arch.kv_bytes_per_token() * ctx_mid
     step_bytes = arch.weight_bytes_per_step() + kv_ctx_bytes
+    # HBM traffic of that kernel from the PMC passes of scripts/pmc_traffic.sh (FETCH_SIZE x2
+    # + WRITE_SIZE per launch, committed under profiles/), when one exists for this shape
+    traffic, traffic_src = None, None
+    if arch.name == "tts1":
+        import glob
+
+        hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{dom}_{B}.json")))
+        if hits:
+            traffic = round(json.load(open(hits[-1]))["hbm_bytes_per_launch"])  # bytes per launch
+            traffic_src = os.path.relpath(hits[-1], ROOT)
     roofline = dict(bound="hbm", kernel=f"wgemm/{dom}" if dom != "attention" else "attn_decode",
                     achieved=round(kern[dom]["gbs"], 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(kern[dom]["gbs"] / HBM_PEAK_GBS, 4), traffic=None,
+                    frac=round(kern[dom]["gbs"] / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
                     bytes_per_launch=kern[dom]["bytes"], avg_launch_ms=round(kern[dom]["avg_ms"], 5),
                     decode_step=dict(ms=round(step_ms, 4), bytes=step_bytes,
                                      achieved_gbs=round(step_bytes / step_ms / 1e6, 1),
