@@ -305,7 +305,10 @@ struct Ctx {
       WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
       const bf16_t* xin = x ? x + (size_t)r0 * K : nullptr;
       bool norm = normw != nullptr;
-      if (norm && (!p.a_lds || p.sliced || K > 4096)) {  // fused RMSNorm: rows in LDS, K <= 4096
+      // fused RMSNorm only where the rows sit in registers (<= 16 rows, the early prologue):
+      // at 17..64 rows every workgroup would normalise every row again — one standalone
+      // pass (same canonical order: identical bits) is cheaper
+      if (norm && (!p.a_lds || p.sliced || K > 4096 || m > 16)) {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
