@@ -3,10 +3,11 @@
 //
 // Reference: tts/core/codec/decoder.py:69-89 (Decoder.forward), decoding.py:84-89
 // (AudioDecoder.decode), decoder_modules.py (Generator / VocosBackbone / ISTFTHead),
-// upsampler.py (UpSamplerBlock).  The reference decodes one utterance per call in fp32;
-// a batch here is a sequence of utterances decoded back to back on one stream (GroupNorm
-// statistics and the unmasked attention span a whole utterance, so utterances must not be
-// padded together: SURVEY Appendix A6).
+// upsampler.py (UpSamplerBlock).  The reference decodes one utterance per call in fp32.
+// GroupNorm statistics and the unmasked attention span a whole utterance, so utterances
+// are never padded together: a batch is spread over kLanes streams,
+// each with its own workspace, and the utterances of different lanes run concurrently
+// (each one alone is far too small to fill 256 CUs).
 #include <math.h>
 #include <string.h>
 
@@ -48,9 +49,25 @@ struct Codec {
   float* window;                             // [nfft]
   int nfft = 0, nb = 0, ldh = 0;
   int cap_T = 0, cap_F = 0;
-  // workspaces
-  DevBuf codes, b0, b1, b2, big, qkv, stats, head, spec, frames, wav;
+  // per-lane workspaces + streams
+  struct Lane {
+    DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    ~Lane() {
+      if (done) (void)hipEventDestroy(done);
+      if (st) (void)hipStreamDestroy(st);
+    }
+  };
+  std::vector<std::unique_ptr<Lane>> lanes;
+  hipEvent_t start = nullptr;
+  DevBuf codes, wav;  // all utterances' codes; host-bound waveforms staged on the device
+  ~Codec() {
+    if (start) (void)hipEventDestroy(start);
+  }
 };
+
+static constexpr int kLanes = 4;  // = the HIP hardware queues per process (GPU_MAX_HW_QUEUES)
 
 void codec_destroy(Codec* c) { delete c; }
 
@@ -255,19 +272,30 @@ void codec_load(Engine* e, const tts_codec_config* cfgp, const tts_tensor_desc* 
   cd->cap_T = Tm;
   cd->cap_F = Fm;
   const size_t rows = (size_t)Fm + 2 * kPad;
-  cd->codes.alloc((size_t)Tm * 4);
-  cd->b0.alloc(rows * D * 4);
-  cd->b1.alloc(rows * D * 4);
-  cd->b2.alloc(rows * D * 4);
   size_t big = std::max((size_t)Tm * 4 * D, (size_t)Tm * VQ);
-  for (auto& u : cd->ups) big = std::max(big, (size_t)Tm * 8 * u.k * u.Cout);  // generous
-  cd->big.alloc(big * 4);
-  cd->qkv.alloc((size_t)Tm * 3 * D * 4);
-  cd->stats.alloc(64 * 2 * 4);
-  cd->head.alloc((size_t)Fm * ldh * 4);
-  cd->spec.alloc((size_t)Fm * ldh * 4);
-  cd->frames.alloc((size_t)Fm * nfft * 4);
-  cd->wav.alloc((size_t)Fm * c.hop_length * 4);
+  {  // ConvTranspose GEMM output Z = [Tc][k*Cout] at each stage's input length
+    int Tc = Tm;
+    for (auto& u : cd->ups) {
+      big = std::max(big, (size_t)Tc * u.k * u.Cout);
+      Tc *= u.u;
+    }
+  }
+  for (int l = 0; l < kLanes; ++l) {
+    auto ln = std::make_unique<Codec::Lane>();
+    ln->b0.alloc(rows * D * 4);
+    ln->b1.alloc(rows * D * 4);
+    ln->b2.alloc(rows * D * 4);
+    ln->big.alloc(big * 4);
+    ln->qkv.alloc((size_t)Tm * 3 * D * 4);
+    ln->stats.alloc(64 * 2 * 4);
+    ln->head.alloc((size_t)Fm * ldh * 4);
+    ln->spec.alloc((size_t)Fm * ldh * 4);
+    ln->frames.alloc((size_t)Fm * nfft * 4);
+    HIP_CHECK(hipStreamCreateWithFlags(&ln->st, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
+    cd->lanes.push_back(std::move(ln));
+  }
+  HIP_CHECK(hipEventCreateWithFlags(&cd->start, hipEventDisableTiming));
   if (e->codec) codec_destroy(e->codec);
   e->codec = cd.release();
 }
@@ -309,87 +337,108 @@ void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, f
   const int D = c.hidden_dim, H = c.heads, VQ = c.vq_dim;
   int ups = 1;
   for (int i = 0; i < c.n_upsample; ++i) ups *= c.upsample_factors[i];
-  size_t off_codes = 0, off_wav = 0;
+  // ---- validate everything before any launch; one upload of all codes
+  size_t n_codes = 0, n_wav = 0;
   for (int b = 0; b < B; ++b) {
     const int T = lens[b];
     TTS_REQUIRE(T >= 1 && T <= cd.cap_T, "utterance length out of range (max_codes)");
     for (int i = 0; i < T; ++i)
-      TTS_REQUIRE(codes[off_codes + i] >= 0 && codes[off_codes + i] < 65536, "code out of range");
+      TTS_REQUIRE(codes[n_codes + i] >= 0 && codes[n_codes + i] < 65536, "code out of range");
+    n_codes += T;
+    n_wav += (size_t)T * ups * c.hop_length;
+  }
+  if (cd.codes.bytes < n_codes * 4) cd.codes.alloc(n_codes * 4);
+  if (!wav_is_device && cd.wav.bytes < n_wav * 4) cd.wav.alloc(n_wav * 4);
+  HIP_CHECK(hipMemcpyAsync(cd.codes.p, codes, n_codes * 4, hipMemcpyHostToDevice, s));
+  float* wav_dev = wav_is_device ? wav : cd.wav.as<float>();
+  const int NL = std::min(B, kLanes);
+  HIP_CHECK(hipEventRecord(cd.start, s));
+  for (int l = 0; l < NL; ++l) HIP_CHECK(hipStreamWaitEvent(cd.lanes[l]->st, cd.start, 0));
+
+  size_t off_codes = 0, off_wav = 0;
+  for (int b = 0; b < B; ++b) {
+    Codec::Lane& ln = *cd.lanes[b % NL];
+    const hipStream_t ls = ln.st;
+    const int T = lens[b];
     const int F = T * ups;
     const size_t rows_cap = (size_t)cd.cap_F + 2 * kPad;
     // zero the padding rows (and everything else) of the three activation buffers
-    launch_zero(cd.b0.as<float>(), (long long)rows_cap * D, s);
-    launch_zero(cd.b1.as<float>(), (long long)rows_cap * D, s);
-    launch_zero(cd.b2.as<float>(), (long long)rows_cap * D, s);
-    HIP_CHECK(hipMemcpyAsync(cd.codes.p, codes + off_codes, (size_t)T * 4, hipMemcpyHostToDevice, s));
-    float* big = cd.big.as<float>();
-    float* b0 = cd.b0.as<float>();
-    float* b1 = cd.b1.as<float>();
-    float* b2 = cd.b2.as<float>();
+    launch_zero(ln.b0.as<float>(), (long long)rows_cap * D, ls);
+    launch_zero(ln.b1.as<float>(), (long long)rows_cap * D, ls);
+    launch_zero(ln.b2.as<float>(), (long long)rows_cap * D, ls);
+    float* big = ln.big.as<float>();
+    float* b0 = ln.b0.as<float>();
+    float* b1 = ln.b1.as<float>();
+    float* b2 = ln.b2.as<float>();
+    float* stats = ln.stats.as<float>();
     auto R = [&](float* buf, int C) { return buf + (size_t)kPad * C; };
     // FSQ -> project_out -> fc_post_a
-    launch_fsq_project(cd.codes.as<int>(), T, cd.po_w, cd.po_b, big, VQ, s);
-    gemm(big, T, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, s);
+    launch_fsq_project(cd.codes.as<int>() + off_codes, T, cd.po_w, cd.po_b, big, VQ, ls);
+    gemm(big, T, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, ls);
     // embed Conv1d(k=7, pad=3): window starts 3 rows above
-    gemm(R(b0, D) - 3 * D, T, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, s);
+    gemm(R(b0, D) - 3 * D, T, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, ls);
     // prior_net: b1 -> b0 -> b1
-    resnet(cd.prior[0], b1, b2, b0, T, cd.stats.as<float>(), s);
-    resnet(cd.prior[1], b0, b2, b1, T, cd.stats.as<float>(), s);
+    resnet(cd.prior[0], b1, b2, b0, T, stats, ls);
+    resnet(cd.prior[1], b0, b2, b1, T, stats, ls);
     // transformers on x = b1 (in place residual stream), scratch b2 / big / qkv
     float* x = R(b1, D);
+    float* qkv = ln.qkv.as<float>();
     for (int l = 0; l < c.depth; ++l) {
       const CodecTfBlock& tb = cd.tf[l];
-      launch_rmsnorm_f32(x, T, D, tb.att_norm, 1e-6f, R(b2, D), s);
-      gemm(R(b2, D), T, D, D, tb.c_attn, 3 * D, nullptr, cd.qkv.as<float>(), 3 * D, nullptr, 0, s);
-      launch_codec_rope(cd.qkv.as<float>(), T, H, D / H, s);
-      launch_codec_attention(cd.qkv.as<float>(), T, H, D / H, R(b2, D), s);
-      gemm(R(b2, D), T, D, D, tb.c_proj, D, nullptr, x, D, x, 0, s);
-      launch_rmsnorm_f32(x, T, D, tb.ffn_norm, 1e-6f, R(b2, D), s);
-      gemm(R(b2, D), T, D, D, tb.fc1, 4 * D, nullptr, big, 4 * D, nullptr, 1, s);
-      gemm(big, T, 4 * D, 4 * D, tb.fc2, D, nullptr, x, D, x, 0, s);
+      launch_rmsnorm_f32(x, T, D, tb.att_norm, 1e-6f, R(b2, D), ls);
+      gemm(R(b2, D), T, D, D, tb.c_attn, 3 * D, nullptr, qkv, 3 * D, nullptr, 0, ls);
+      launch_codec_rope(qkv, T, H, D / H, ls);
+      launch_codec_attention(qkv, T, H, D / H, R(b2, D), ls);
+      gemm(R(b2, D), T, D, D, tb.c_proj, D, nullptr, x, D, x, 0, ls);
+      launch_rmsnorm_f32(x, T, D, tb.ffn_norm, 1e-6f, R(b2, D), ls);
+      gemm(R(b2, D), T, D, D, tb.fc1, 4 * D, nullptr, big, 4 * D, nullptr, 1, ls);
+      gemm(big, T, 4 * D, 4 * D, tb.fc2, D, nullptr, x, D, x, 0, ls);
     }
     // post_net: b1 -> b0 -> b1
-    resnet(cd.post[0], b1, b2, b0, T, cd.stats.as<float>(), s);
-    resnet(cd.post[1], b0, b2, b1, T, cd.stats.as<float>(), s);
-    launch_layernorm_f32(R(b1, D), T, D, cd.ln_w, cd.ln_b, 1e-6f, R(b0, D), s);
+    resnet(cd.post[0], b1, b2, b0, T, stats, ls);
+    resnet(cd.post[1], b0, b2, b1, T, stats, ls);
+    launch_layernorm_f32(R(b1, D), T, D, cd.ln_w, cd.ln_b, 1e-6f, R(b0, D), ls);
     float* hid = R(b0, D);  // [T][D]
     int Tc = T, C = D;
     float* cur = b0;
     for (size_t i = 0; i < cd.ups.size(); ++i) {
       const CodecUp& u = cd.ups[i];
-      gemm(R(cur, C), Tc, u.Cin, u.Cin, u.wz, u.k * u.Cout, nullptr, big, u.k * u.Cout, nullptr, 0, s);
+      gemm(R(cur, C), Tc, u.Cin, u.Cin, u.wz, u.k * u.Cout, nullptr, big, u.k * u.Cout, nullptr, 0, ls);
       float* nxt = (cur == b0) ? b1 : b0;
       // clear stale rows of the destination so the padding below is zero again
-      launch_zero(nxt, (long long)rows_cap * D, s);
-      launch_convt_gather(big, Tc, u.Cout, u.k, u.u, u.pad, u.bias, R(nxt, u.Cout), s);
+      launch_zero(nxt, (long long)rows_cap * D, ls);
+      launch_convt_gather(big, Tc, u.Cout, u.k, u.u, u.pad, u.bias, R(nxt, u.Cout), ls);
       Tc *= u.u;
       C = u.Cout;
-      launch_zero(b2, (long long)rows_cap * D, s);
+      launch_zero(b2, (long long)rows_cap * D, ls);
       float* res_out = (nxt == b0) ? b1 : b0;
-      launch_zero(res_out, (long long)rows_cap * D, s);
-      resnet(u.rb, nxt, b2, res_out, Tc, cd.stats.as<float>(), s);
+      launch_zero(res_out, (long long)rows_cap * D, ls);
+      resnet(u.rb, nxt, b2, res_out, Tc, stats, ls);
       cur = res_out;
     }
     if (!cd.ups.empty()) {
       float* dst = (cur == b0) ? b1 : b0;
-      gemm(R(cur, C), Tc, C, C, cd.out_w, D, cd.out_b, R(dst, D), D, nullptr, 1, s);
+      gemm(R(cur, C), Tc, C, C, cd.out_w, D, cd.out_b, R(dst, D), D, nullptr, 1, ls);
       hid = R(dst, D);
     }
     // ISTFT head
-    gemm(hid, F, D, D, cd.head_w, cd.ldh, cd.head_b, cd.head.as<float>(), cd.ldh, nullptr, 0, s);
-    launch_istft_spec(cd.head.as<float>(), F, cd.nb, cd.ldh, cd.spec.as<float>(), s);
-    gemm(cd.spec.as<float>(), F, cd.ldh, cd.ldh, cd.basis, cd.nfft, nullptr, cd.frames.as<float>(),
-         cd.nfft, nullptr, 0, s);
-    float* wout = wav_is_device ? wav + off_wav : cd.wav.as<float>();
-    launch_ola(cd.frames.as<float>(), F, cd.nfft, c.hop_length, cd.window, wout, s);
+    gemm(hid, F, D, D, cd.head_w, cd.ldh, cd.head_b, ln.head.as<float>(), cd.ldh, nullptr, 0, ls);
+    launch_istft_spec(ln.head.as<float>(), F, cd.nb, cd.ldh, ln.spec.as<float>(), ls);
+    gemm(ln.spec.as<float>(), F, cd.ldh, cd.ldh, cd.basis, cd.nfft, nullptr, ln.frames.as<float>(),
+         cd.nfft, nullptr, 0, ls);
+    launch_ola(ln.frames.as<float>(), F, cd.nfft, c.hop_length, cd.window, wav_dev + off_wav, ls);
     HIP_CHECK(hipGetLastError());
     const size_t L = (size_t)F * c.hop_length;
-    if (!wav_is_device)
-      HIP_CHECK(hipMemcpyAsync(wav + off_wav, wout, L * 4, hipMemcpyDeviceToHost, s));
     wav_lens[b] = (int64_t)L;
     off_codes += T;
     off_wav += L;
   }
+  // join the lanes back into the caller's stream
+  for (int l = 0; l < NL; ++l) {
+    HIP_CHECK(hipEventRecord(cd.lanes[l]->done, cd.lanes[l]->st));
+    HIP_CHECK(hipStreamWaitEvent(s, cd.lanes[l]->done, 0));
+  }
+  if (!wav_is_device) HIP_CHECK(hipMemcpyAsync(wav, wav_dev, n_wav * 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
