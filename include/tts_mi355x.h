@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TTS_ABI_VERSION 1
+#define TTS_ABI_VERSION 2
 
 typedef int32_t tts_status;
 enum {
@@ -114,6 +114,9 @@ typedef struct {
   float top_p;                 /* sampling only                                      */
   int32_t top_k;               /* sampling only (HF default 50); 0 = off             */
   uint64_t seed;               /* sampling RNG seed                                  */
+  float frequency_penalty;     /* vLLM form (inferencing.py:85): logit -= f * count of */
+                               /* the id among the NEW tokens; 0 = off (HF form)       */
+  int32_t reserved;
 } tts_gen_params;
 
 /* Runs prefill + the autoregressive decode loop for `batch` independent sequences.

@@ -183,3 +183,26 @@ def sample_probs(scores: torch.Tensor, temperature: float, top_k: int, top_p: fl
         rm[-1:] = False
         s = s.masked_fill(rm.scatter(0, si, rm), float("-inf"))
     return torch.softmax(s, dim=-1)
+
+
+def vllm_process(scores: torch.Tensor, prompt: list[int], output: list[int], repetition_penalty: float,
+                 frequency_penalty: float, min_tokens: int, stop_id: int) -> torch.Tensor:
+    """vLLM's penalties for the vLLM form of the reference call (inferencing.py:75-92:
+    repetition_penalty, frequency_penalty, min_tokens, stop_token_ids), restated from vLLM's
+    `apply_penalties` (vllm/model_executor/layers/utils.py; vLLM is not installed here and
+    the reference pins no version of it, so this restatement is PARITY UNPINNED):
+    repetition over ids in prompt | output (logits > 0 ? /p : *p), then
+    `logits -= frequency_penalty * count(id in output)`, and the stop id masked while
+    len(output) < min_tokens (MinTokensLogitsProcessor)."""
+    s = scores.float().clone()
+    seen = sorted(set(prompt) | set(output))
+    if repetition_penalty != 1.0 and seen:
+        idx = torch.tensor(seen, dtype=torch.long)
+        g = s[idx]
+        s[idx] = torch.where(g > 0, g / repetition_penalty, g * repetition_penalty)
+    if frequency_penalty != 0.0 and output:
+        cnt = torch.bincount(torch.tensor(output, dtype=torch.long), minlength=s.numel()).float()
+        s = s - frequency_penalty * cnt
+    if stop_id >= 0 and len(output) < min_tokens:
+        s[stop_id] = float("-inf")
+    return s

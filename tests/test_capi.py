@@ -31,7 +31,7 @@ def test_abi_version_and_error_path():
     from tts_amd import _lib
 
     lib = _lib.load_library()
-    assert lib.tts_abi_version() == 1
+    assert lib.tts_abi_version() == 2
     # invalid argument path: no GPU work, error message set, status non-zero
     st = lib.tts_engine_create(0, None)
     assert st != 0
@@ -43,6 +43,6 @@ def test_struct_layouts_match_header():
 
     # sizes follow the C declarations (all 4-byte fields except the uint64 seed / int64 shape)
     assert ctypes.sizeof(_lib.LmConfig) == 17 * 4
-    assert ctypes.sizeof(_lib.GenParams) == 8 * 4 + 8
+    assert ctypes.sizeof(_lib.GenParams) == 8 * 4 + 8 + 2 * 4  # + frequency_penalty, reserved (ABI 2)
     assert ctypes.sizeof(_lib.CodecConfig) == (4 + 8 + 5) * 4
     assert ctypes.sizeof(_lib.TensorDesc) == 8 + 8 + 4 + 4 + 32 + 8

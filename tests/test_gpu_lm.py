@@ -194,3 +194,35 @@ def test_batched_decode_tts1_dims(rows):
         for o in outs:
             assert o == outs[0]
         assert outs[0][:k] == ref[:k], (k, outs[0], ref)
+
+
+def test_vllm_form_frequency_penalty():
+    """vLLM-form greedy with the reference's vLLM defaults (repetition 1.1 — CLI 1.4 —,
+    frequency 0.3/0.4, min_tokens): teacher-forced on the engine's own output, every pick is
+    the argmax of the oracle's restatement of vLLM's penalties (parity unpinned: vLLM is
+    not installed) wherever the top-2 margin clears the logit tolerance."""
+    arch, seed, cases = _cases("lm_tiny")
+    m = _model(arch, seed)
+    c = cases[0]
+
+    class SP:
+        max_tokens = 40
+        min_tokens = 12
+        stop_token_ids = [c["eos"]]
+        repetition_penalty = 1.4
+        frequency_penalty = 0.4
+        temperature = 0.0
+
+    new = m.generate(prompt_token_ids=c["prompt"], sampling_params=SP())[0].outputs[0].token_ids
+    assert 12 <= len(new) <= 40
+    plain = m.generate_batch([c["prompt"]], max_length=len(c["prompt"]) + 40, min_new_tokens=12,
+                             eos_token_id=c["eos"], repetition_penalty=1.4)[0]
+    assert new != plain  # the frequency penalty changes the greedy path
+    seq = c["prompt"] + new
+    lg = m.score([seq], len(new) + 1)[0]
+    P = len(c["prompt"])
+    for i in range(len(new)):
+        sc = lm_oracle.vllm_process(lg[i], c["prompt"], new[:i], 1.4, 0.4, 12, c["eos"])
+        top = torch.topk(sc, 2).values
+        if float(top[0] - top[1]) >= LOGIT_TOL:
+            assert int(torch.argmax(sc)) == new[i], i

@@ -86,6 +86,7 @@ struct LmWork {
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
+  DevBuf counts;                                    // vLLM frequency penalty: new-token counts [B][V] u16
   DevBuf logits;                                    // scoring output (bf16)
   DevBuf row_slot, row_pos, row_idx;                // prefill row descriptors
   DevBuf st_int;                                    // step-state ints
@@ -102,6 +103,7 @@ struct LmWork {
   int graph_sample = -1, graph_top_k = -1;
   float graph_temp = -1.f, graph_top_p = -1.f;
   unsigned long long graph_seed = 0;
+  float graph_freq = 0.f;
   int* h_active = nullptr;  // pinned host copy of n_active (ring of 2)
 };
 

@@ -249,6 +249,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
     w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
   }
   w.slogits.alloc((size_t)B * V * 4);
+  w.counts.alloc((size_t)B * (V / 32 + 1) * 32 * 2);
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.row_slot.alloc((size_t)R * 4);
@@ -399,6 +400,7 @@ struct Ctx {
     st.n_active = base + 6 * B;
     st.seen = w.seen.as<uint32_t>();
     st.seen_stride = c.vocab_size / 32 + 1;
+    st.counts = nullptr;
     st.out_ids = w.out_ids.as<int>();
     st.out_stride = w.out_cap;
     st.eos_id = eos;
@@ -415,6 +417,7 @@ struct Ctx {
     ex.part_val = w.lpart_v.as<float>(); ex.part_idx = w.lpart_i.as<int>();
     ex.part_stride = LOGITS_MAX_PARTS;
     if (gp.do_sample) { ex.logits_out = w.slogits.as<float>(); ex.ldl = c.vocab_size; }
+    ex.counts = st.counts; ex.freq_penalty = gp.frequency_penalty;
     TTS_REQUIRE(B <= kPrefillChunk, "batch larger than one GEMM chunk");
     WgemmPlan p = plan_wgemm(B, c.vocab_size, c.hidden_size, EPI_LOGITS, e->num_cu);
     gemm(xin, B, c.hidden_size, M.lm_head, c.vocab_size, M.final_norm, nullptr, 0, nullptr,
@@ -502,6 +505,11 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
   }
   st_host[6 * B] = B;
   StepState st = X.state(B, p->eos_token_id, p->min_new_tokens);
+  TTS_REQUIRE(std::isfinite(p->frequency_penalty), "frequency_penalty must be finite");
+  if (p->frequency_penalty != 0.f) {  // vLLM form: counts of the new tokens only
+    st.counts = e->w.counts.as<uint16_t>();
+    HIP_CHECK(hipMemsetAsync(st.counts, 0, (size_t)B * st.seen_stride * 32 * 2, s));
+  }
   HIP_CHECK(hipMemcpyAsync(e->w.st_int.p, st_host.data(), st_host.size() * 4,
                            hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(e->w.seen.p, seen.data(), seen.size() * 4, hipMemcpyHostToDevice, s));
@@ -538,7 +546,8 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
   const bool smp_changed =
       W.graph_sample != p->do_sample ||
       (p->do_sample && (W.graph_temp != p->temperature || W.graph_top_k != p->top_k ||
-                        W.graph_top_p != p->top_p || W.graph_seed != p->seed));
+                        W.graph_top_p != p->top_p || W.graph_seed != p->seed)) ||
+      W.graph_freq != p->frequency_penalty;
   if (W.graph && (W.graph_batch != B || W.graph_pen != pen || W.graph_eos != p->eos_token_id ||
                   W.graph_min_new != p->min_new_tokens || smp_changed)) {
     hipGraphExecDestroy(e->w.graph);
@@ -563,6 +572,7 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
     W.graph_top_k = p->top_k;
     W.graph_top_p = p->top_p;
     W.graph_seed = p->seed;
+    W.graph_freq = p->frequency_penalty;
   }
   Engine::Gen& G = e->gen;
   G.open = true;

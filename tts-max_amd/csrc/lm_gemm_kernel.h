@@ -561,6 +561,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             float v = rbf(acc[0][mt][r]);  // logits are materialised in bf16, then .float()
             const uint32_t bits = seen_cur[mt][r];
             if ((bits >> (n & 31)) & 1u) v = (v < 0.f) ? v * a.penalty : v / a.penalty;
+            if (a.counts) v -= a.freq_penalty * (float)a.counts[(size_t)m * a.seen_stride * 32 + n];
             if (n == eosr[mt][r]) v = -INFINITY;
             if (a.logits_out) a.logits_out[(size_t)m * a.ldl + n] = v;
             argmax_merge(best_v[mt][r], best_i[mt][r], v, n);

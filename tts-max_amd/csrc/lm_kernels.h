@@ -65,6 +65,8 @@ struct WgemmArgs {
   const int* attn_pos = nullptr;
   int attn_split = 0, attn_nsplit = 0, attn_D = 0;
   float* logits_out = nullptr;  // EPI_LOGITS: also store the processed fp32 logits [M][ldl] (sampling)
+  const uint16_t* counts = nullptr;  // EPI_LOGITS: new-token counts [M][seen_stride*32] (frequency penalty)
+  float freq_penalty = 0.f;
   int ldl = 0;
   int ur = 0;         // layout: units per round (StreamPlan::ur, filled in by launch_wgemm)
   int kc = 1;         // layout: K chunks (StreamPlan::kc, filled in by launch_wgemm)
@@ -190,6 +192,7 @@ struct StepState {
   int* out_ids;       // [B][out_stride]
   int out_stride;
   int* n_active;      // [1]
+  uint16_t* counts;   // [B][V] new-token counts (frequency penalty) or nullptr
   int eos_id;
   int min_new;
 };

@@ -100,6 +100,7 @@ __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* 
     st.out_ids[(size_t)b * st.out_stride + g] = tok;
     st.gen_count[b] = g + 1;
     st.seen[(size_t)b * st.seen_stride + (tok >> 5)] |= 1u << (tok & 31);
+    if (st.counts) st.counts[(size_t)b * st.seen_stride * 32 + tok] += 1;
     st.tokens[b] = tok;
     st.pos[b] += 1;
     const bool stop = (tok == st.eos_id) || (g + 1 >= st.limit[b]);

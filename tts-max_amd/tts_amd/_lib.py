@@ -97,6 +97,8 @@ class GenParams(ctypes.Structure):
         ("top_p", ctypes.c_float),
         ("top_k", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("frequency_penalty", ctypes.c_float),
+        ("reserved", ctypes.c_int32),
     ]
 
 

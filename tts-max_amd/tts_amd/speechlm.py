@@ -177,7 +177,7 @@ class MI355XSpeechLM:
     def generate_batch(self, prompts: Sequence[Sequence[int]], max_length: int, min_new_tokens: int = 0,
                        eos_token_id: int = -1, do_sample: bool = False, repetition_penalty: float = 1.0,
                        top_p: float = 1.0, temperature: float = 1.0, top_k: int | None = None,
-                       seed: int | None = None) -> list[list[int]]:
+                       seed: int | None = None, frequency_penalty: float = 0.0) -> list[list[int]]:
         """Independent sequences (each as its batch-1 HF generate): returns new tokens.
 
         do_sample: GenerationMixin._sample's warpers (temperature, top_k — HF default 50 —,
@@ -201,7 +201,7 @@ class MI355XSpeechLM:
         params = _lib.GenParams(max_length=max_length, min_new_tokens=min_new_tokens, eos_token_id=eos_token_id,
                                 do_sample=1 if do_sample else 0, repetition_penalty=repetition_penalty,
                                 temperature=temperature, top_p=top_p, top_k=50 if top_k is None else top_k,
-                                seed=0 if seed is None else seed)
+                                seed=0 if seed is None else seed, frequency_penalty=frequency_penalty)
         pi32 = ctypes.POINTER(ctypes.c_int32)
         _lib.check(self._lib.tts_generate(self._h, ctypes.byref(params), flat.ctypes.data_as(pi32),
                                           lens.ctypes.data_as(pi32), B, out.ctypes.data_as(pi32), stride,
@@ -248,8 +248,8 @@ class MI355XSpeechLM:
     def _generate_vllm_form(self, prompt_token_ids, sampling_params):
         sp = sampling_params
         temperature = float(getattr(sp, "temperature", 1.0) or 0.0)
-        if temperature > 0 and float(getattr(sp, "frequency_penalty", 0.0) or 0.0) != 0.0:
-            raise NotImplementedError("vLLM frequency_penalty is not implemented (HF-form sampling is)")
+        if float(getattr(sp, "presence_penalty", 0.0) or 0.0) != 0.0:
+            raise NotImplementedError("vLLM presence_penalty is not implemented")
         top_k = int(getattr(sp, "top_k", -1) or -1)
         if temperature > 0 and top_k <= 0:
             raise NotImplementedError("full-vocabulary sampling (vLLM top_k=-1) is not built; pass top_k")
@@ -263,7 +263,8 @@ class MI355XSpeechLM:
                                   do_sample=temperature > 0, temperature=temperature or 1.0,
                                   top_p=float(getattr(sp, "top_p", 1.0)),
                                   top_k=top_k if top_k > 0 else None,
-                                  seed=getattr(sp, "seed", None))[0]
+                                  seed=getattr(sp, "seed", None),
+                                  frequency_penalty=float(getattr(sp, "frequency_penalty", 0.0) or 0.0))[0]
         return [RequestOutput(prompt_token_ids=prompt, outputs=[CompletionOutput(token_ids=new)])]
 
     # ------------------------------------------------------------------ utilities ------
