@@ -79,3 +79,28 @@ def test_batch_equals_single_and_oracle():
     dev = dec.decode_batch(utts, out=out)
     for b, d in zip(batch, dev):
         assert np.array_equal(d.cpu().numpy(), b)
+
+
+def test_decode_split_from_reference_codes_format(tmp_path):
+    """Batched voicing of a stored split (codes_io.decode_split) == one decode per utterance."""
+    from tts_amd import codes_io, configs
+    from tts_amd.codec import MI355XAudioDecoder
+
+    zc = np.load(os.path.join(GOLDEN, "codec_24k_d2.npz"))
+    carch = configs.CODEC_ARCHS[str(zc["arch"])]
+    dec = MI355XAudioDecoder.synthetic(carch, seed=int(zc["seed"]), max_codes=64)
+    rng = np.random.default_rng(1)
+    utts = [rng.integers(0, 65536, n).tolist() for n in (9, 30, 64, 70, 3, 12)]
+    codes_io.write_codes(str(tmp_path / "ds"), "val", utts)
+    st = codes_io.decode_split(dec, str(tmp_path / "ds"), "val", str(tmp_path / "out"), batch=4)
+    assert st == {"utterances": 6, "voiced": 5, "skipped": 1,
+                  "samples": sum(len(u) for u in utts if len(u) <= 64) * carch.samples_per_code}
+    wav = np.fromfile(tmp_path / "out" / "val_wav.f32", dtype=np.float32)
+    index = np.load(tmp_path / "out" / "val_wav_index.npy")
+    assert index[3] == -1
+    for i, u in enumerate(utts):
+        if len(u) > 64:
+            continue
+        one = dec.decode(torch.tensor(u))[0].numpy()
+        assert np.array_equal(wav[index[i]:index[i] + one.shape[0]], one)
+    dec.close()

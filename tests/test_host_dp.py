@@ -115,3 +115,22 @@ def test_dp_world2_gloo_equals_single(balance):
     prompts = [[i] * (1 + i % 5) for i in range(11)]
     ref = [[t * 2 + len(p) for t in p] + [len(p)] for p in prompts]
     assert out == ref
+
+
+def test_codes_format_roundtrip_matches_reference_reader(tmp_path):
+    """tts_amd.codes_io reads the reference's layout (raw int32 memmap + np.save'd offsets,
+    data_vectorizer.py:122-146 / data_utils.py:106-148) back exactly."""
+    import numpy as np
+
+    from tts_amd import codes_io
+
+    rng = np.random.default_rng(0)
+    utts = [rng.integers(0, 65536, n).tolist() for n in (5, 1, 17, 40)]
+    codes_io.write_codes(str(tmp_path), "train", utts, rank=3)
+    # the reference reader's arithmetic, verbatim in spirit: memmap + index spans
+    raw = np.memmap(tmp_path / "train_codes_3.npy", dtype=np.int32, mode="r")
+    idx = np.load(tmp_path / "train_codes_index_3.npy")
+    assert idx.tolist() == [0, 5, 6, 23] and raw.shape[0] == 63
+    codes, spans = codes_io.read_codes(str(tmp_path), "train", rank=3)
+    assert [codes[l:r].tolist() for l, r in spans] == utts
+    assert list(codes_io.batches(spans, 2, 20)) == [[0, 1], [2]]  # 40 > max_codes: skipped
