@@ -301,8 +301,12 @@ struct Ctx {
       launch_pgemm(a, epi, e->num_cu, s);
       return;
     }
-    for (int r0 = 0; r0 < rows; r0 += kPrefillChunk) {
-      const int m = std::min(kPrefillChunk, rows - r0);
+    // decode GEMV launches hold at most 32 rows (two m-tiles: the A rows fit LDS); 33..64
+    // rows run as two launches (the weights stream twice, still far cheaper than A rows
+    // read from global memory)
+    const int chunk = rows > 32 ? 32 : kPrefillChunk;
+    for (int r0 = 0; r0 < rows; r0 += chunk) {
+      const int m = std::min(chunk, rows - r0);
       WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
       const bf16_t* xin = x ? x + (size_t)r0 * K : nullptr;
       bool norm = normw != nullptr;
@@ -315,7 +319,17 @@ struct Ctx {
         norm = false;
       }
       WgemmArgs a;
-      if (logit_extra) a = *logit_extra;
+      if (logit_extra) {
+        a = *logit_extra;
+        if (r0 > 0) {  // per-row operands of the lm_head epilogue start at row r0
+          if (a.seen) a.seen += (size_t)r0 * a.seen_stride;
+          if (a.eos_mask) a.eos_mask += r0;
+          if (a.part_val) a.part_val += (size_t)r0 * a.part_stride;
+          if (a.part_idx) a.part_idx += (size_t)r0 * a.part_stride;
+          if (a.logits_out) a.logits_out += (size_t)r0 * a.ldl;
+          if (a.counts) a.counts += (size_t)r0 * a.seen_stride * 32;
+        }
+      }
       a.x = xin; a.M = m; a.K = K; a.ldx = K;
       a.w = W; a.N = N;
       a.normw = normw; a.eps = c.rms_norm_eps;
@@ -443,14 +457,14 @@ struct Ctx {
 static void check_launch() { HIP_CHECK(hipGetLastError()); }
 
 // Prefill a group of sequences [b0, b0+nb): rows = sum of their prompt lengths.
-static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, int B,
+static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, int B, int slot_base,
                                std::vector<int>& last_rows, int& rows) {
   std::vector<int> slot, pos, tok;
   rows = 0;
   last_rows.resize(B);
   for (int b = 0; b < B; ++b) {
     for (int i = 0; i < lens[b]; ++i) {
-      slot.push_back(b);
+      slot.push_back(slot_base + b);
       pos.push_back(i);
       tok.push_back(ids[rows + i]);
     }
@@ -517,13 +531,25 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
   HIP_CHECK(hipEventRecord(e->ev[2], s));
 
   // ---- prefill
-  std::vector<int> last_rows;
-  int rows = 0;
-  prefill_rows_setup(X, ids, lens, B, last_rows, rows);
-  X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
-  HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, last_rows.data(), B * 4, hipMemcpyHostToDevice, s));
-  launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, e->w.row_idx.as<int>(),
-                     e->w.last_x.as<bf16_t>(), B, c.hidden_size, s);
+  // groups of whole prompts that fit the prefill workspace, each in one pass
+  {
+    std::vector<int> last_rows;
+    int b0 = 0;
+    size_t id_off = 0;
+    while (b0 < B) {
+      int b1 = b0, grp_rows = 0;
+      while (b1 < B && grp_rows + lens[b1] <= e->w.cap_rows) grp_rows += lens[b1++];
+      TTS_REQUIRE(b1 > b0, "a prompt is longer than the prefill workspace");
+      int rows = 0;
+      prefill_rows_setup(X, ids + id_off, lens + b0, b1 - b0, b0, last_rows, rows);
+      X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
+      HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, last_rows.data(), (b1 - b0) * 4, hipMemcpyHostToDevice, s));
+      launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, e->w.row_idx.as<int>(),
+                         e->w.last_x.as<bf16_t>() + (size_t)b0 * c.hidden_size, b1 - b0, c.hidden_size, s);
+      id_off += grp_rows;
+      b0 = b1;
+    }
+  }
   X.head_and_pick(e->w.last_x.as<bf16_t>(), B, st, *p);
   check_launch();
   HIP_CHECK(hipEventRecord(e->ev[3], s));
@@ -755,7 +781,7 @@ void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_l
   }
   std::vector<int> last_rows;
   int rows = 0;
-  prefill_rows_setup(X, ids, lens, B, last_rows, rows);
+  prefill_rows_setup(X, ids, lens, B, 0, last_rows, rows);
   X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
   // gather the last n_last rows of every sequence
   std::vector<int> sel;
