@@ -114,11 +114,10 @@ def main():
             prompts = [mine[i, 1:1 + int(mine[i, 0])].tolist() for i in range(B)]
         new = lm.generate_batch(prompts, max_length=P + N, min_new_tokens=N, eos_token_id=vocab.speech_end_id,
                                 repetition_penalty=1.1)
-        # codec input = prompt speech codes + generated codes (ids -> codes via the LUT)
-        utts = []
-        for p, n in zip(prompts, new):
-            codes = [c for c in lm.ids_to_codes(p[-args.prompt_codes:] + n) if c >= 0]
-            utts.append(codes)
+        # codec input = prompt speech codes + generated codes.  Random-init weights emit
+        # non-speech ids too (a trained TTS-1 emits speech codes); every generated token is
+        # voiced as one code (synthetic_codes) so the codec workload has the configured size
+        utts = [synthetic_codes(lm, p[-args.prompt_codes:] + n) for p, n in zip(prompts, new)]
         wav = dec.decode_batch(utts, out=wav_buf)
         if local_prompts is not None:
             return sum(len(n) for n in new), wav
@@ -217,8 +216,8 @@ def main():
         from tts_amd.streaming import StreamingSynthesizer
 
         p8 = p32[:8]
-        pc8 = [[c for c in lm.ids_to_codes(p[-args.prompt_codes:]) if c >= 0] for p in p8]
-        ss = StreamingSynthesizer(lm, dec, chunk=25, left_context=25)
+        pc8 = [synthetic_codes(lm, p[-args.prompt_codes:]) for p in p8]
+        ss = StreamingSynthesizer(lm, dec, chunk=25, left_context=25, to_codes=lambda ids: synthetic_codes(lm, ids))
         firsts, totals = [], []
         for r in range(3):
             first = None
@@ -272,6 +271,12 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def synthetic_codes(lm, ids):
+    """Speech codes of `ids` through the LUT; a non-speech id (emitted by random weights)
+    stands for the code id % 65536, so every token is voiced."""
+    return [c if c >= 0 else i % 65536 for i, c in zip(ids, lm.ids_to_codes(ids))]
 
 
 def cpu_baseline(arch, carch, prompt, N, args):

@@ -52,9 +52,13 @@ struct Codec {
   // per-lane workspaces + streams
   struct Lane {
     DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
+    DevBuf gcodes, gwav;  // fixed input / output of the lane's captured graphs
+    DevBuf kpart;         // split-K GEMM partials
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr;
+    std::map<int, hipGraphExec_t> graphs;  // one captured decode per utterance length
     ~Lane() {
+      for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
       if (done) (void)hipEventDestroy(done);
       if (st) (void)hipStreamDestroy(st);
     }
@@ -68,6 +72,9 @@ struct Codec {
 };
 
 static constexpr int kLanes = 4;  // = the HIP hardware queues per process (GPU_MAX_HW_QUEUES)
+static constexpr size_t kSplitElems = (size_t)4 << 20;  // split-K partial floats per lane
+// workspace of the lane whose launch sequence is being enqueued (decode_one)
+static thread_local float* t_split_ws = nullptr;
 
 void codec_destroy(Codec* c) { delete c; }
 
@@ -291,6 +298,9 @@ void codec_load(Engine* e, const tts_codec_config* cfgp, const tts_tensor_desc* 
     ln->head.alloc((size_t)Fm * ldh * 4);
     ln->spec.alloc((size_t)Fm * ldh * 4);
     ln->frames.alloc((size_t)Fm * nfft * 4);
+    ln->gcodes.alloc((size_t)Tm * 4);
+    ln->kpart.alloc(kSplitElems * 4);
+    ln->gwav.alloc((size_t)Fm * c.hop_length * 4);
     HIP_CHECK(hipStreamCreateWithFlags(&ln->st, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
     cd->lanes.push_back(std::move(ln));
@@ -307,6 +317,7 @@ void gemm(const float* A, int M, int K, int lda, const float* B, int N, const fl
   GemmF32Args g;
   g.A = A; g.M = M; g.K = K; g.lda = lda; g.B = B; g.N = N; g.bias = bias;
   g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
+  g.part = t_split_ws; g.part_elems = t_split_ws ? kSplitElems : 0;
   launch_gemm_f32(g, s);
 }
 
@@ -329,37 +340,15 @@ void resnet(const CodecResBlock& rb, float* x, float* tmp, float* out, int T, fl
 
 }  // namespace
 
-void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, float* wav,
-                  int wav_is_device, int64_t* wav_lens, hipStream_t s) {
-  TTS_REQUIRE(e->codec != nullptr, "tts_codec_load has not been called");
-  Codec& cd = *e->codec;
+// The whole Decoder.forward launch sequence of one utterance of T codes on lane `ln`
+// (stream `ls`): codes_in [T] int32 (device) -> wav_out [T * samples_per_code] f32 (device).
+static void decode_one(Codec& cd, Codec::Lane& ln, int T, const int* codes_in, float* wav_out,
+                       hipStream_t ls) {
   const tts_codec_config& c = cd.cfg;
   const int D = c.hidden_dim, H = c.heads, VQ = c.vq_dim;
   int ups = 1;
   for (int i = 0; i < c.n_upsample; ++i) ups *= c.upsample_factors[i];
-  // ---- validate everything before any launch; one upload of all codes
-  size_t n_codes = 0, n_wav = 0;
-  for (int b = 0; b < B; ++b) {
-    const int T = lens[b];
-    TTS_REQUIRE(T >= 1 && T <= cd.cap_T, "utterance length out of range (max_codes)");
-    for (int i = 0; i < T; ++i)
-      TTS_REQUIRE(codes[n_codes + i] >= 0 && codes[n_codes + i] < 65536, "code out of range");
-    n_codes += T;
-    n_wav += (size_t)T * ups * c.hop_length;
-  }
-  if (cd.codes.bytes < n_codes * 4) cd.codes.alloc(n_codes * 4);
-  if (!wav_is_device && cd.wav.bytes < n_wav * 4) cd.wav.alloc(n_wav * 4);
-  HIP_CHECK(hipMemcpyAsync(cd.codes.p, codes, n_codes * 4, hipMemcpyHostToDevice, s));
-  float* wav_dev = wav_is_device ? wav : cd.wav.as<float>();
-  const int NL = std::min(B, kLanes);
-  HIP_CHECK(hipEventRecord(cd.start, s));
-  for (int l = 0; l < NL; ++l) HIP_CHECK(hipStreamWaitEvent(cd.lanes[l]->st, cd.start, 0));
-
-  size_t off_codes = 0, off_wav = 0;
-  for (int b = 0; b < B; ++b) {
-    Codec::Lane& ln = *cd.lanes[b % NL];
-    const hipStream_t ls = ln.st;
-    const int T = lens[b];
+  t_split_ws = ln.kpart.as<float>();
     const int F = T * ups;
     const size_t rows_cap = (size_t)cd.cap_F + 2 * kPad;
     // zero the padding rows (and everything else) of the three activation buffers
@@ -373,7 +362,7 @@ void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, f
     float* stats = ln.stats.as<float>();
     auto R = [&](float* buf, int C) { return buf + (size_t)kPad * C; };
     // FSQ -> project_out -> fc_post_a
-    launch_fsq_project(cd.codes.as<int>() + off_codes, T, cd.po_w, cd.po_b, big, VQ, ls);
+    launch_fsq_project(codes_in, T, cd.po_w, cd.po_b, big, VQ, ls);
     gemm(big, T, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, ls);
     // embed Conv1d(k=7, pad=3): window starts 3 rows above
     gemm(R(b0, D) - 3 * D, T, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, ls);
@@ -426,9 +415,65 @@ void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, f
     launch_istft_spec(ln.head.as<float>(), F, cd.nb, cd.ldh, ln.spec.as<float>(), ls);
     gemm(ln.spec.as<float>(), F, cd.ldh, cd.ldh, cd.basis, cd.nfft, nullptr, ln.frames.as<float>(),
          cd.nfft, nullptr, 0, ls);
-    launch_ola(ln.frames.as<float>(), F, cd.nfft, c.hop_length, cd.window, wav_dev + off_wav, ls);
-    HIP_CHECK(hipGetLastError());
-    const size_t L = (size_t)F * c.hop_length;
+    launch_ola(ln.frames.as<float>(), F, cd.nfft, c.hop_length, cd.window, wav_out, ls);
+  HIP_CHECK(hipGetLastError());
+}
+
+void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, float* wav,
+                  int wav_is_device, int64_t* wav_lens, hipStream_t s) {
+  TTS_REQUIRE(e->codec != nullptr, "tts_codec_load has not been called");
+  Codec& cd = *e->codec;
+  const tts_codec_config& c = cd.cfg;
+  int ups = 1;
+  for (int i = 0; i < c.n_upsample; ++i) ups *= c.upsample_factors[i];
+  // ---- validate everything before any launch; one upload of all codes
+  size_t n_codes = 0, n_wav = 0;
+  for (int b = 0; b < B; ++b) {
+    const int T = lens[b];
+    TTS_REQUIRE(T >= 1 && T <= cd.cap_T, "utterance length out of range (max_codes)");
+    for (int i = 0; i < T; ++i)
+      TTS_REQUIRE(codes[n_codes + i] >= 0 && codes[n_codes + i] < 65536, "code out of range");
+    n_codes += T;
+    n_wav += (size_t)T * ups * c.hop_length;
+  }
+  if (cd.codes.bytes < n_codes * 4) cd.codes.alloc(n_codes * 4);
+  if (!wav_is_device && cd.wav.bytes < n_wav * 4) cd.wav.alloc(n_wav * 4);
+  HIP_CHECK(hipMemcpyAsync(cd.codes.p, codes, n_codes * 4, hipMemcpyHostToDevice, s));
+  float* wav_dev = wav_is_device ? wav : cd.wav.as<float>();
+  const int NL = std::min(B, kLanes);
+  HIP_CHECK(hipEventRecord(cd.start, s));
+  for (int l = 0; l < NL; ++l) HIP_CHECK(hipStreamWaitEvent(cd.lanes[l]->st, cd.start, 0));
+
+  // Each utterance replays its lane's graph for that length (captured on first use): ~150
+  // launches become one, which is what makes short streaming windows cheap.  The graph
+  // reads / writes the lane's fixed buffers; two device copies move codes and samples.
+  size_t off_codes = 0, off_wav = 0;
+  for (int b = 0; b < B; ++b) {
+    Codec::Lane& ln = *cd.lanes[b % NL];
+    const int T = lens[b];
+    const size_t L = (size_t)T * ups * c.hop_length;
+    auto it = ln.graphs.find(T);
+    if (it == ln.graphs.end()) {
+      if (ln.graphs.size() >= 32) {  // bounded cache: drop the smallest length
+        (void)hipGraphExecDestroy(ln.graphs.begin()->second);
+        ln.graphs.erase(ln.graphs.begin());
+      }
+      hipStream_t cs;
+      HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+      hipGraph_t g;
+      HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+      decode_one(cd, ln, T, ln.gcodes.as<int>(), ln.gwav.as<float>(), cs);
+      HIP_CHECK(hipStreamEndCapture(cs, &g));
+      hipGraphExec_t ge;
+      HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      HIP_CHECK(hipGraphDestroy(g));
+      HIP_CHECK(hipStreamDestroy(cs));
+      it = ln.graphs.emplace(T, ge).first;
+    }
+    HIP_CHECK(hipMemcpyAsync(ln.gcodes.p, cd.codes.as<int>() + off_codes, (size_t)T * 4,
+                             hipMemcpyDeviceToDevice, ln.st));
+    HIP_CHECK(hipGraphLaunch(it->second, ln.st));
+    HIP_CHECK(hipMemcpyAsync(wav_dev + off_wav, ln.gwav.p, L * 4, hipMemcpyDeviceToDevice, ln.st));
     wav_lens[b] = (int64_t)L;
     off_codes += T;
     off_wav += L;

@@ -17,6 +17,11 @@ struct GemmF32Args {
   int ldc = 0;
   const float* resid = nullptr;  // [M][ldc]
   int act = 0;                   // 0 none, 1 swish/silu
+  // split-K over workgroups (short utterances / streaming windows: few output tiles, long
+  // K): fp32 partials [ksplit][M][N] in `part`, summed in split order by a reduce kernel
+  float* part = nullptr;
+  size_t part_elems = 0;  // capacity of `part`
+  int ksplit = 1, kchunk = 0;
 };
 void launch_gemm_f32(const GemmF32Args& g, hipStream_t s);
 

@@ -10,6 +10,8 @@
 // so a Conv1d(k) over a zero-padded buffer is a plain GEMM whose A operand is a sliding
 // window: row t starts at x + (t - k/2)*C and spans k*C contiguous floats (lda = C < K).
 // No im2col buffer is ever written.
+#include <algorithm>
+
 #include "codec_kernels.h"
 #include "hip_common.h"
 
@@ -36,6 +38,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int nbn = (g.N + TN - 1) / TN;
   const int m0 = (blockIdx.x / nbn) * TM, n0 = (blockIdx.x % nbn) * TN;
+  const int kbeg = blockIdx.y * g.kchunk;  // split-K range (kchunk = K when not split)
+  const int kend = min(g.K, kbeg + g.kchunk);
   // staging map: thread -> (row, 4*AV consecutive k)
   const int arow = t / (GBK / (4 * AV)), ak = (t % (GBK / (4 * AV))) * 4 * AV;
   const int brow = t / (GBK / (4 * BV)), bk = (t % (GBK / (4 * BV))) * 4 * BV;
@@ -43,8 +47,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
   const bool aok = ar < g.M, bok = br < g.N;
   // out-of-range rows read a clamped (valid) row and are zeroed after the load: a load
   // inside a branch makes hipcc wait on it before the next one is issued
-  const float* ap = g.A + (size_t)(aok ? ar : g.M - 1) * g.lda + ak;
-  const float* bp = g.B + (size_t)(bok ? br : g.N - 1) * g.K + bk;
+  const float* ap = g.A + (size_t)(aok ? ar : g.M - 1) * g.lda + kbeg + ak;
+  const float* bp = g.B + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk;
   f32x16_t acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
     const float4 l = *(const float4*)(bp + 4 * v);
     rb[v] = bok ? l : z4;
   }
-  for (int k0 = 0; k0 < g.K; k0 += GBK) {
+  for (int k0 = kbeg; k0 < kend; k0 += GBK) {
     __syncthreads();
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
@@ -82,8 +86,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
       Bs[(bk + 4 * v + 3) * LSB + brow] = rb[v].w;
     }
     __syncthreads();
-    if (k0 + GBK < g.K) {  // prefetch next K tile while the MFMAs run
-      const int kn = k0 + GBK;
+    if (k0 + GBK < kend) {  // prefetch next K tile while the MFMAs run
+      const int kn = k0 + GBK - kbeg;
 #pragma unroll
       for (int v = 0; v < AV; ++v) {
         const float4 l = *(const float4*)(ap + kn + 4 * v);
@@ -122,6 +126,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (TM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= g.M) continue;
+        if (g.ksplit > 1) {  // raw partial; bias / act / residual in the reduce
+          g.part[((size_t)blockIdx.y * g.M + m) * g.N + n] = acc[i][j][r];
+          continue;
+        }
         float v = acc[i][j][r] + bias;
         if (g.act == 1) v = v / (1.0f + expf(-v));
         if (g.resid) v = g.resid[(size_t)m * g.ldc + n] + v;
@@ -130,14 +138,50 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
   }
 }
 
-void launch_gemm_f32(const GemmF32Args& g, hipStream_t s) {
+__global__ void gemm_f32_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                       const float* __restrict__ bias, int act, const float* resid,
+                                       float* C, int ldc) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)M * N) return;
+  const int m = (int)(i / N), n = (int)(i % N);
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[((size_t)s * M + m) * N + n];
+  if (bias) v += bias[n];
+  if (act == 1) v = v / (1.0f + expf(-v));
+  if (resid) v = resid[(size_t)m * ldc + n] + v;
+  C[(size_t)m * ldc + n] = v;
+}
+
+void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
+  GemmF32Args g = g_in;
   const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
   if (big >= 256) {
+    g.ksplit = 1; g.kchunk = g.K;
     hipLaunchKernelGGL((gemm_f32_kernel<128, 128>), dim3(big), dim3(256), 0, s, g);
-  } else {
-    const int grid = ((g.M + 63) / 64) * ((g.N + 63) / 64);
-    hipLaunchKernelGGL((gemm_f32_kernel<64, 64>), dim3(grid), dim3(256), 0, s, g);
+    return;
   }
+  const int grid = ((g.M + 63) / 64) * ((g.N + 63) / 64);
+  // split K when the tiles cannot fill the chip and K is long (the K loop is serial per
+  // workgroup): up to 16 splits of >= 256 columns, bounded by the partial workspace
+  int S = 1;
+  if (g.part != nullptr && grid < 192 && g.K >= 512) {
+    S = std::min(16, std::max(1, 256 / grid));
+    S = std::min(S, g.K / 256);
+    while (S > 1 && (size_t)S * g.M * g.N > g.part_elems) --S;
+  }
+  if (S <= 1) {
+    g.ksplit = 1; g.kchunk = g.K;
+    hipLaunchKernelGGL((gemm_f32_kernel<64, 64>), dim3(grid), dim3(256), 0, s, g);
+    return;
+  }
+  g.ksplit = S;
+  g.kchunk = ((g.K + S - 1) / S + GBK - 1) / GBK * GBK;
+  S = (g.K + g.kchunk - 1) / g.kchunk;
+  g.ksplit = S;
+  hipLaunchKernelGGL((gemm_f32_kernel<64, 64>), dim3(grid, S), dim3(256), 0, s, g);
+  const long long n = (long long)g.M * g.N;
+  hipLaunchKernelGGL(gemm_f32_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g.part, S,
+                     g.M, g.N, g.bias, g.act, g.resid, g.C, g.ldc);
 }
 
 // ------------------------------------------------------------------ small kernels -----

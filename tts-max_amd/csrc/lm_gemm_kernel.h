@@ -138,7 +138,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   float4 poe[CPG][2];
   int pose = 0;
   if constexpr (early_o) {
-    {
+    if (!(a.diag & 64)) {
       const int it = tid % aitems, grp = min(tid / aitems, agroups - 1);
       const int D = a.attn_D, H = a.K / D;
       const int m = it / kch, hd = (it - m * kch) * 8;

@@ -27,8 +27,12 @@ import numpy as np
 
 
 class StreamingSynthesizer:
-    def __init__(self, lm, codec, chunk: int = 25, left_context: int = 25):
+    def __init__(self, lm, codec, chunk: int = 25, left_context: int = 25, to_codes=None):
+        """to_codes(ids) -> speech codes of a row's new ids; default: the LUT of the
+        checkpoint tokenizer, non-speech ids dropped (extract_speech_ids,
+        inferencing.py:53-63)."""
         self.lm, self.codec = lm, codec
+        self.to_codes = to_codes or (lambda ids: [c for c in lm.ids_to_codes(ids) if c >= 0])
         self.chunk, self.left = chunk, left_context
         self.spc = codec.sample_rate // codec.token_rate
 
@@ -44,7 +48,7 @@ class StreamingSynthesizer:
             """One window per row with a full chunk pending (or any codes, when flushing)."""
             wins, rows, emit = [], [], []
             for b in range(B):
-                codes = [c for c in self.lm.ids_to_codes(new_ids[b]) if c >= 0]
+                codes = self.to_codes(new_ids[b])
                 pending = len(codes) - voiced[b]
                 if pending >= self.chunk or (flush and pending > 0):
                     n = min(self.chunk, pending)
