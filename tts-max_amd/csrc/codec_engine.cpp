@@ -232,7 +232,7 @@ void codec_load(Engine* e, const tts_codec_config* cfgp, const tts_tensor_desc* 
   // ---- ISTFT head and its irfft basis
   const int nfft = 4 * c.hop_length;  // Generator: n_fft = hop_length * 4
   const int nb = nfft / 2 + 1;
-  const int ldh = (2 * nb + 15) & ~15;
+  const int ldh = (2 * nb + 63) & ~63;  // K of the basis GEMM: a multiple of its K step
   cd->nfft = nfft; cd->nb = nb; cd->ldh = ldh;
   {
     const tts_tensor_desc& hw = tm.get("decoder.head.out.weight", {nfft + 2, D});

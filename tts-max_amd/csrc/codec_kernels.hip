@@ -24,9 +24,7 @@ namespace tts {
 // MFMA operand read is 32 consecutive floats.  The next K tile is loaded into registers
 // while the current one is consumed.  64x64 tiles are used when 128x128 would leave CUs
 // idle (the codec's T ~ 500-2000 rows).
-constexpr int GBK = 16;
-
-template <int TM, int TN>
+template <int TM, int TN, int GBK>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
   constexpr int LSA = TM + 2, LSB = TN + 2;
   constexpr int AV = TM * GBK / 256 / 4;  // float4 per thread for the A tile (1 or 2)
@@ -152,36 +150,49 @@ __global__ void gemm_f32_reduce_kernel(const float* __restrict__ part, int S, in
   C[(size_t)m * ldc + n] = v;
 }
 
-void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
-  GemmF32Args g = g_in;
-  const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
-  if (big >= 256) {
-    g.ksplit = 1; g.kchunk = g.K;
-    hipLaunchKernelGGL((gemm_f32_kernel<128, 128>), dim3(big), dim3(256), 0, s, g);
-    return;
-  }
-  const int grid = ((g.M + 63) / 64) * ((g.N + 63) / 64);
-  // split K when the tiles cannot fill the chip and K is long (the K loop is serial per
-  // workgroup): up to 16 splits of >= 256 columns, bounded by the partial workspace
+// K step per barrier pair: 64 (64x64 tiles) / 32 (128x128) where K allows — enough MFMA
+// work per step to cover the next step's L2 latency; 16 otherwise
+template <int TM, int TN>
+static void launch_tile(const GemmF32Args& g, dim3 grid, hipStream_t s) {
+  constexpr int BIG = TM == 128 ? 32 : 64;
+  if (g.kchunk % BIG == 0 && g.K % BIG == 0)
+    hipLaunchKernelGGL((gemm_f32_kernel<TM, TN, BIG>), grid, dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<TM, TN, 16>), grid, dim3(256), 0, s, g);
+}
+
+// Tiles: 128x128 (4 waves x 2x2 MFMA accumulators, K step 32) when that grid fills the
+// chip, else 64x64 split over K up to ~768 workgroups (measured best at T = 650: 128x128
+// tiles split to the same count were 25 % slower).
+template <int TM, int TN>
+static void launch_split(GemmF32Args g, int target, hipStream_t s) {
+  const int grid = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
   int S = 1;
-  if (g.part != nullptr && grid < 192 && g.K >= 512) {
-    S = std::min(16, std::max(1, 256 / grid));
+  if (g.part != nullptr && grid < target * 3 / 4 && g.K >= 512) {
+    S = std::min(16, std::max(1, (target + grid - 1) / grid));
     S = std::min(S, g.K / 256);
     while (S > 1 && (size_t)S * g.M * g.N > g.part_elems) --S;
   }
   if (S <= 1) {
     g.ksplit = 1; g.kchunk = g.K;
-    hipLaunchKernelGGL((gemm_f32_kernel<64, 64>), dim3(grid), dim3(256), 0, s, g);
+    launch_tile<TM, TN>(g, dim3(grid), s);
     return;
   }
-  g.ksplit = S;
-  g.kchunk = ((g.K + S - 1) / S + GBK - 1) / GBK * GBK;
+  const int step = (g.K % 64 == 0) ? 64 : 16;
+  g.kchunk = ((g.K + S - 1) / S + step - 1) / step * step;
   S = (g.K + g.kchunk - 1) / g.kchunk;
   g.ksplit = S;
-  hipLaunchKernelGGL((gemm_f32_kernel<64, 64>), dim3(grid, S), dim3(256), 0, s, g);
+  launch_tile<TM, TN>(g, dim3(grid, S), s);
   const long long n = (long long)g.M * g.N;
   hipLaunchKernelGGL(gemm_f32_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g.part, S,
                      g.M, g.N, g.bias, g.act, g.resid, g.C, g.ldc);
+}
+
+void launch_gemm_f32(const GemmF32Args& g, hipStream_t s) {
+  static const int target = getenv("TTS_CODEC_SPLIT_TARGET") ? atoi(getenv("TTS_CODEC_SPLIT_TARGET")) : 768;
+  const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+  if (big >= 256) launch_split<128, 128>(g, target, s);
+  else launch_split<64, 64>(g, target, s);
 }
 
 // ------------------------------------------------------------------ small kernels -----
