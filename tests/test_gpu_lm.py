@@ -226,3 +226,24 @@ def test_vllm_form_frequency_penalty():
         top = torch.topk(sc, 2).values
         if float(top[0] - top[1]) >= LOGIT_TOL:
             assert int(torch.argmax(sc)) == new[i], i
+
+
+def test_rows_stop_at_different_steps():
+    """A batch whose rows hit EOS at different steps: stopped rows idle inside the captured
+    step (their kernels skip them) while the others continue; every row equals its batch-1
+    run, EOS included, and lengths differ."""
+    arch, seed, cases = _cases("lm_small")
+    m = _model(arch, seed)
+    prompts = [c["prompt"] for c in cases]
+    L = max(len(p) for p in prompts) + 40
+    free = m.generate_batch(prompts, max_length=L, min_new_tokens=0, eos_token_id=-1, repetition_penalty=1.1)
+    # a token some row emits for the first time (step >= 1 where the row varies): it stops there; the
+    # others stop when (if) they emit it
+    r, i = next((r, k) for r in range(len(free)) for k in range(len(free[r])) if free[r][k] not in free[r][:k] and k >= (1 if len(set(free[r])) > 1 else 0))
+    eos = free[r][i]
+    batch = m.generate_batch(prompts, max_length=L, min_new_tokens=0, eos_token_id=eos, repetition_penalty=1.1)
+    singles = [m.generate_batch([p], max_length=L, min_new_tokens=0, eos_token_id=eos, repetition_penalty=1.1)[0]
+               for p in prompts]
+    assert batch == singles
+    assert batch[r] == free[r][:i + 1]
+    assert len({len(x) for x in batch}) > 1 or len(batch) == 1
