@@ -144,6 +144,23 @@ tts_status tts_generate_begin(tts_engine* e, const tts_gen_params* p, const int3
 tts_status tts_generate_continue(tts_engine* e, int32_t n_steps, int32_t* all_done);
 tts_status tts_generate_read(tts_engine* e, int32_t* out_ids, int32_t out_stride, int32_t* out_lens);
 
+/* Continuous batching (serving): `n_slots` persistent decode rows share
+ * one captured decode step and the settings `p` (max_length ignored).  A sequence is
+ * admitted into a free slot between steps (tts_slots_add: prompt prefilled into that
+ * slot, first token picked; max_new_tokens bounds it like HF max_length - prompt length),
+ * tts_slots_step runs `n_steps` decode steps over all slots (*n_active = rows still
+ * generating), tts_slots_read returns a slot's new tokens so far and whether it stopped,
+ * tts_slots_release frees the slot (stopping it first if it is still running).  Each
+ * sequence's tokens equal a batch-1 tts_generate of its prompt with the same settings
+ * (rows never mix).  Opening slots discards an open tts_generate_begin generation. */
+tts_status tts_slots_open(tts_engine* e, const tts_gen_params* p, int32_t n_slots, void* stream);
+tts_status tts_slots_add(tts_engine* e, int32_t slot, const int32_t* prompt_ids, int32_t prompt_len,
+                         int32_t max_new_tokens);
+tts_status tts_slots_step(tts_engine* e, int32_t n_steps, int32_t* n_active);
+tts_status tts_slots_read(tts_engine* e, int32_t slot, int32_t* out_ids, int32_t capacity, int32_t* n_out,
+                          int32_t* finished);
+tts_status tts_slots_release(tts_engine* e, int32_t slot);
+
 /* Teacher-forced scoring (parity / debugging): runs the prefill over full sequences and
  * writes the bf16-rounded logits of the last `n_last` positions of each sequence, as
  * fp32, to host `logits` [batch][n_last][vocab]. */

@@ -1,0 +1,74 @@
+"""Continuous batching (tts_slots_*): requests admitted into free rows between decode chunks
+and retired when they stop give exactly their batch-1 tokens."""
+
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _model():
+    from tts_amd import configs
+    from tts_amd.speechlm import MI355XSpeechLM
+
+    z = np.load(os.path.join(GOLDEN, "lm_small.npz"))
+    arch = configs.LM_ARCHS[str(z["arch"])]
+    return MI355XSpeechLM.synthetic(arch, seed=int(z["seed"]), max_batch=4, max_seq_len=512), z
+
+
+def test_continuous_batching_equals_batch1():
+    from tts_amd.serving import ContinuousBatcher
+
+    m, z = _model()
+    rng = np.random.default_rng(3)
+    base = z["prompt_ids"][:int(z["prompt_lens"][0])].tolist()
+    V = m.arch.vocab_size
+    prompts = [base[:n] + rng.integers(0, V, 5).tolist() for n in (10, 40, 7, 25, 60, 3, 33)]
+    max_new = [12, 30, 5, 18, 9, 26, 14]
+    free = m.generate_batch([prompts[0]], max_length=len(prompts[0]) + 30, eos_token_id=-1, repetition_penalty=1.1)[0]
+    eos = free[len(free) // 2]  # some rows stop on EOS before their max_new
+    ref = [m.generate_batch([p], max_length=len(p) + n, min_new_tokens=2, eos_token_id=eos,
+                            repetition_penalty=1.1)[0] for p, n in zip(prompts, max_new)]
+    b = ContinuousBatcher(m, n_slots=3, eos_token_id=eos, min_new_tokens=2, repetition_penalty=1.1, chunk=4)
+    got = b.generate(prompts, max_new)  # 7 requests through 3 rows
+    assert got == ref
+    # background-thread serving, requests submitted while others run
+    b2 = ContinuousBatcher(m, n_slots=2, eos_token_id=eos, min_new_tokens=2, repetition_penalty=1.1, chunk=3)
+    b2.start()
+    futs = [b2.submit(p, n) for p, n in zip(prompts, max_new)]
+    assert [f.result(timeout=60) for f in futs] == ref
+    b2.close()
+    m.close()
+
+
+def test_vllm_shaped_llm_and_http_app():
+    from fastapi.testclient import TestClient
+
+    from tts_amd.serving import LLM, ContinuousBatcher, create_app
+
+    m, z = _model()
+    p = z["prompt_ids"][:int(z["prompt_lens"][0])].tolist()
+
+    class SP:
+        max_tokens = 12
+        min_tokens = 3
+        stop_token_ids = [-1]
+        repetition_penalty = 1.1
+        temperature = 0.0
+
+    ref = m.generate_batch([p], max_length=len(p) + 12, min_new_tokens=3, eos_token_id=-1, repetition_penalty=1.1)[0]
+    llm = LLM(m, n_slots=2)
+    out = llm.generate(prompt_token_ids=p, sampling_params=SP())
+    assert out[0].outputs[0].token_ids == ref
+    outs = llm.generate(prompt_token_ids=[p, p[:20]], sampling_params=SP())
+    assert outs[0].outputs[0].token_ids == ref and len(outs[1].outputs[0].token_ids) == 12
+    b = ContinuousBatcher(m, n_slots=2, min_new_tokens=3, repetition_penalty=1.1)
+    with TestClient(create_app(b)) as client:
+        r = client.post("/generate", json={"prompt_token_ids": p, "max_tokens": 12})
+        assert r.status_code == 200 and r.json()["token_ids"] == ref
+        assert client.post("/generate", json={"prompt_token_ids": [], "max_tokens": 3}).status_code == 400
+    b.close()
+    m.close()

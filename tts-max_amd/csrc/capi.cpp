@@ -128,6 +128,53 @@ tts_status tts_generate_read(tts_engine* e, int32_t* out_ids, int32_t out_stride
   });
 }
 
+tts_status tts_slots_open(tts_engine* e, const tts_gen_params* p, int32_t n_slots, void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(e && p, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_slots_open(E, p, n_slots, pick_stream(E, stream));
+  });
+}
+
+tts_status tts_slots_add(tts_engine* e, int32_t slot, const int32_t* prompt_ids, int32_t prompt_len,
+                         int32_t max_new_tokens) {
+  return guarded([&] {
+    TTS_REQUIRE(e && prompt_ids, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_slots_add(E, slot, prompt_ids, prompt_len, max_new_tokens);
+  });
+}
+
+tts_status tts_slots_step(tts_engine* e, int32_t n_steps, int32_t* n_active) {
+  return guarded([&] {
+    TTS_REQUIRE(e && n_active && n_steps >= 0, "bad argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    *n_active = lm_slots_step(E, n_steps);
+  });
+}
+
+tts_status tts_slots_read(tts_engine* e, int32_t slot, int32_t* out_ids, int32_t capacity, int32_t* n_out,
+                          int32_t* finished) {
+  return guarded([&] {
+    TTS_REQUIRE(e && out_ids && n_out && finished, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_slots_read(E, slot, out_ids, capacity, n_out, finished);
+  });
+}
+
+tts_status tts_slots_release(tts_engine* e, int32_t slot) {
+  return guarded([&] {
+    TTS_REQUIRE(e, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_slots_release(E, slot);
+  });
+}
+
 tts_status tts_lm_score(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
                         int32_t n_last, float* logits, void* stream) {
   return guarded([&] {

@@ -126,6 +126,15 @@ struct Engine {
     bool finished = false;
     hipStream_t s = nullptr;
   } gen;
+  // continuous batching (tts_slots_*): S persistent rows, sequences admitted / retired
+  // between decode chunks
+  struct Slots {
+    bool open = false;
+    int S = 0;
+    tts_gen_params gp{};
+    std::vector<int> busy;  // 1 while a sequence owns the slot (until released)
+    hipStream_t s = nullptr;
+  } slots;
   ~Engine();
 };
 
@@ -139,6 +148,11 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
                   hipStream_t s);
 int lm_gen_continue(Engine* e, int n_steps);
 void lm_gen_read(Engine* e, int32_t* out_ids, int out_stride, int32_t* out_lens);
+void lm_slots_open(Engine* e, const tts_gen_params* p, int S, hipStream_t s);
+void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_new);
+int lm_slots_step(Engine* e, int n_steps);
+void lm_slots_read(Engine* e, int slot, int32_t* out_ids, int cap, int32_t* n_out, int32_t* finished);
+void lm_slots_release(Engine* e, int slot);
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
               float* logits, hipStream_t s);
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,

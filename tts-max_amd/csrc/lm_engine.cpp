@@ -479,9 +479,54 @@ static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, 
                X.c.hidden_size, X.s);
 }
 
+// The decode step (all layers + lm_head + pick + finalize over B rows) captured once into a
+// hipGraph.  The graph bakes in B, the penalty, eos/min_new and the sampling parameters
+// (kernel arguments): recaptured when any of them changes.
+static void ensure_step_graph(Engine* e, int B, const StepState& st, const tts_gen_params& gp) {
+  LmWork& W = e->w;
+  const tts_gen_params* p = &gp;
+  const float pen = p->repetition_penalty;
+  const bool smp_changed =
+      W.graph_sample != p->do_sample ||
+      (p->do_sample && (W.graph_temp != p->temperature || W.graph_top_k != p->top_k ||
+                        W.graph_top_p != p->top_p || W.graph_seed != p->seed)) ||
+      W.graph_freq != p->frequency_penalty;
+  if (W.graph && (W.graph_batch != B || W.graph_pen != pen || W.graph_eos != p->eos_token_id ||
+                  W.graph_min_new != p->min_new_tokens || smp_changed)) {
+    (void)hipGraphExecDestroy(W.graph);
+    W.graph = nullptr;
+  }
+  if (W.graph) return;
+  auto step = [&](hipStream_t ss) {
+    Ctx Y(e, ss);
+    Y.layers(B, W.row_slot.as<int>(), st.pos, true);
+    Y.head_and_pick(W.x.as<bf16_t>(), B, st, gp);
+  };
+  hipStream_t cs;
+  HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  hipGraph_t g;
+  HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+  step(cs);
+  HIP_CHECK(hipStreamEndCapture(cs, &g));
+  HIP_CHECK(hipGraphInstantiate(&W.graph, g, nullptr, nullptr, 0));
+  HIP_CHECK(hipGraphDestroy(g));
+  HIP_CHECK(hipStreamDestroy(cs));
+  W.graph_batch = B;
+  W.graph_pen = pen;
+  W.graph_eos = p->eos_token_id;
+  W.graph_min_new = p->min_new_tokens;
+  W.graph_sample = p->do_sample;
+  W.graph_temp = p->temperature;
+  W.graph_top_k = p->top_k;
+  W.graph_top_p = p->top_p;
+  W.graph_seed = p->seed;
+  W.graph_freq = p->frequency_penalty;
+}
+
 void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const int32_t* lens, int B,
                   hipStream_t s) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
+  e->slots.open = false;
   TTS_REQUIRE(p != nullptr && ids != nullptr && lens != nullptr, "null argument");
   TTS_REQUIRE(B >= 1 && B <= e->w.cap_batch, "batch out of range");
   if (p->do_sample) {  // HF: TemperatureLogitsWarper requires T > 0; top_k from GenerationConfig (50)
@@ -559,47 +604,7 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
   for (int b = 0; b < B; ++b) ident[b] = b;
   HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, ident.data(), B * 4, hipMemcpyHostToDevice, s));
   // (the embedding of each sequence's next token is already in w.x rows 0..B-1)
-  const float pen = p->repetition_penalty;
-  const tts_gen_params gp = *p;
-  auto step = [&](hipStream_t ss) {
-    Ctx Y(e, ss);
-    Y.layers(B, e->w.row_slot.as<int>(), st.pos, true);
-    Y.head_and_pick(e->w.x.as<bf16_t>(), B, st, gp);
-  };
-  // the graph bakes in B, the penalty, eos/min_new and the sampling parameters (kernel
-  // args): recapture on change
-  LmWork& W = e->w;
-  const bool smp_changed =
-      W.graph_sample != p->do_sample ||
-      (p->do_sample && (W.graph_temp != p->temperature || W.graph_top_k != p->top_k ||
-                        W.graph_top_p != p->top_p || W.graph_seed != p->seed)) ||
-      W.graph_freq != p->frequency_penalty;
-  if (W.graph && (W.graph_batch != B || W.graph_pen != pen || W.graph_eos != p->eos_token_id ||
-                  W.graph_min_new != p->min_new_tokens || smp_changed)) {
-    hipGraphExecDestroy(e->w.graph);
-    e->w.graph = nullptr;
-  }
-  if (!e->w.graph) {
-    hipStream_t cs;
-    HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-    hipGraph_t g;
-    HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    step(cs);
-    HIP_CHECK(hipStreamEndCapture(cs, &g));
-    HIP_CHECK(hipGraphInstantiate(&e->w.graph, g, nullptr, nullptr, 0));
-    HIP_CHECK(hipGraphDestroy(g));
-    HIP_CHECK(hipStreamDestroy(cs));
-    W.graph_batch = B;
-    W.graph_pen = pen;
-    W.graph_eos = p->eos_token_id;
-    W.graph_min_new = p->min_new_tokens;
-    W.graph_sample = p->do_sample;
-    W.graph_temp = p->temperature;
-    W.graph_top_k = p->top_k;
-    W.graph_top_p = p->top_p;
-    W.graph_seed = p->seed;
-    W.graph_freq = p->frequency_penalty;
-  }
+  ensure_step_graph(e, B, st, *p);
   Engine::Gen& G = e->gen;
   G.open = true;
   G.B = B;
@@ -677,6 +682,158 @@ void lm_generate(Engine* e, const tts_gen_params* p, const int32_t* ids, const i
   e->t_prefill_ms = t0;
   e->t_decode_ms = t1;
   e->gen.open = false;
+}
+
+// ---------------------------------------------------------------- continuous batching --
+// S persistent rows (slots) share one captured decode step; a sequence is admitted into a
+// free slot between chunks (its prompt prefilled into that slot's KV strip, its first token
+// picked, its step-state row initialised) and retired when it stops.  Rows never mix, so
+// every sequence's tokens equal a batch-1 generate of its prompt with the shared settings.
+static void validate_gen_params(const tts_gen_params* p) {
+  TTS_REQUIRE(p != nullptr, "null argument");
+  if (p->do_sample) {
+    TTS_REQUIRE(p->temperature > 0.f, "sampling needs temperature > 0 (temperature 0 = greedy)");
+    TTS_REQUIRE(p->top_k >= 1 && p->top_k <= SAMPLE_MAX_TOP_K,
+                "sampling supports top_k in [1, 1024] (HF default 50; full-vocabulary sampling is not built)");
+    TTS_REQUIRE(p->top_p > 0.f && p->top_p <= 1.f, "top_p must be in (0, 1]");
+  }
+  TTS_REQUIRE(std::isfinite(p->frequency_penalty), "frequency_penalty must be finite");
+}
+
+static StepState slots_state(Engine* e, hipStream_t s) {
+  Engine::Slots& Z = e->slots;
+  StepState st = Ctx(e, s).state(Z.S, Z.gp.eos_token_id, Z.gp.min_new_tokens);
+  if (Z.gp.frequency_penalty != 0.f) st.counts = e->w.counts.as<uint16_t>();
+  return st;
+}
+
+void lm_slots_open(Engine* e, const tts_gen_params* p, int S, hipStream_t s) {
+  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
+  validate_gen_params(p);
+  TTS_REQUIRE(S >= 1 && S <= e->w.cap_batch, "slot count out of range (max_batch)");
+  e->gen.open = false;
+  Engine::Slots& Z = e->slots;
+  Z.open = true;
+  Z.S = S;
+  Z.gp = *p;
+  Z.busy.assign(S, 0);
+  Z.s = s;
+  const int V = e->lm.cfg.vocab_size;
+  // every row idle: done = 1, n_active = 0, no EOS mask
+  std::vector<int> st_host(7 * S + 1, 0);
+  for (int b = 0; b < S; ++b) { st_host[4 * S + b] = 1; st_host[5 * S + b] = -1; }
+  HIP_CHECK(hipMemcpyAsync(e->w.st_int.p, st_host.data(), st_host.size() * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemsetAsync(e->w.seen.p, 0, (size_t)S * (V / 32 + 1) * 4, s));
+  std::vector<int> ident(S);
+  for (int b = 0; b < S; ++b) ident[b] = b;
+  HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, ident.data(), S * 4, hipMemcpyHostToDevice, s));
+  const StepState st = slots_state(e, s);
+  ensure_step_graph(e, S, st, Z.gp);
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_new) {
+  Engine::Slots& Z = e->slots;
+  TTS_REQUIRE(Z.open, "no slot batch open (tts_slots_open)");
+  TTS_REQUIRE(slot >= 0 && slot < Z.S && !Z.busy[slot], "slot out of range or busy");
+  TTS_REQUIRE(prompt != nullptr && len >= 1, "empty prompt");
+  const tts_lm_config& c = e->lm.cfg;
+  const int V = c.vocab_size;
+  TTS_REQUIRE(max_new >= 1 && len + max_new <= c.max_seq_len && max_new <= e->w.out_cap,
+              "prompt + max new tokens exceed max_seq_len");
+  TTS_REQUIRE(len <= e->w.cap_rows, "prompt longer than the prefill workspace");
+  const hipStream_t s = Z.s;
+  Ctx X(e, s);
+  StepState st = slots_state(e, s);
+  const int S = Z.S, stride = st.seen_stride;
+  // ---- the slot's step-state row (and its penalty set) on the device
+  std::vector<uint32_t> seen((size_t)stride, 0u);
+  for (int i = 0; i < len; ++i) {
+    TTS_REQUIRE(prompt[i] >= 0 && prompt[i] < V, "token id out of range");
+    seen[prompt[i] >> 5] |= 1u << (prompt[i] & 31);
+  }
+  HIP_CHECK(hipMemcpyAsync(st.seen + (size_t)slot * stride, seen.data(), (size_t)stride * 4,
+                           hipMemcpyHostToDevice, s));
+  if (st.counts) HIP_CHECK(hipMemsetAsync(st.counts + (size_t)slot * stride * 32, 0, (size_t)stride * 32 * 2, s));
+  const int row[6] = {0, len - 1, 0, max_new, 0, (Z.gp.min_new_tokens > 0) ? Z.gp.eos_token_id : -1};
+  int* base = e->w.st_int.as<int>();
+  for (int k = 0; k < 6; ++k)  // tokens, pos, gen_count, limit, done, eos_mask
+    HIP_CHECK(hipMemcpyAsync(base + k * S + slot, &row[k], 4, hipMemcpyHostToDevice, s));
+  int act = 0;
+  HIP_CHECK(hipMemcpyAsync(&act, st.n_active, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  ++act;
+  HIP_CHECK(hipMemcpyAsync(st.n_active, &act, 4, hipMemcpyHostToDevice, s));
+  // ---- prefill the prompt into the slot's KV strip, pick its first token
+  std::vector<int> last_rows;
+  int rows = 0;
+  prefill_rows_setup(X, prompt, &len, 1, slot, last_rows, rows);
+  X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
+  HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, last_rows.data(), 4, hipMemcpyHostToDevice, s));
+  launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, e->w.row_idx.as<int>(), e->w.last_x.as<bf16_t>(), 1,
+                     c.hidden_size, s);
+  StepState one = st;  // the slot's row as a batch of 1
+  one.tokens += slot; one.pos += slot; one.gen_count += slot; one.limit += slot;
+  one.done += slot; one.eos_mask += slot;
+  one.seen += (size_t)slot * stride;
+  one.out_ids += (size_t)slot * one.out_stride;
+  if (one.counts) one.counts += (size_t)slot * stride * 32;
+  X.head_and_pick(e->w.last_x.as<bf16_t>(), 1, one, Z.gp);
+  // the prefill overwrote the decode rows of w.x: re-embed every row's next token
+  std::vector<int> ident(S);
+  for (int b = 0; b < S; ++b) ident[b] = b;
+  HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, ident.data(), S * 4, hipMemcpyHostToDevice, s));
+  launch_embed(st.tokens, e->lm.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), S, c.hidden_size, s);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(s));
+  Z.busy[slot] = 1;
+}
+
+int lm_slots_step(Engine* e, int n_steps) {
+  Engine::Slots& Z = e->slots;
+  TTS_REQUIRE(Z.open, "no slot batch open (tts_slots_open)");
+  const StepState st = slots_state(e, Z.s);
+  for (int n = 0; n < n_steps; ++n) HIP_CHECK(hipGraphLaunch(e->w.graph, Z.s));
+  int act = 0;
+  HIP_CHECK(hipMemcpyAsync(&act, st.n_active, 4, hipMemcpyDeviceToHost, Z.s));
+  HIP_CHECK(hipStreamSynchronize(Z.s));
+  return act;
+}
+
+void lm_slots_read(Engine* e, int slot, int32_t* out_ids, int cap, int32_t* n_out, int32_t* finished) {
+  Engine::Slots& Z = e->slots;
+  TTS_REQUIRE(Z.open, "no slot batch open (tts_slots_open)");
+  TTS_REQUIRE(slot >= 0 && slot < Z.S, "slot out of range");
+  const StepState st = slots_state(e, Z.s);
+  int gc = 0, dn = 0;
+  HIP_CHECK(hipMemcpyAsync(&gc, st.gen_count + slot, 4, hipMemcpyDeviceToHost, Z.s));
+  HIP_CHECK(hipMemcpyAsync(&dn, st.done + slot, 4, hipMemcpyDeviceToHost, Z.s));
+  HIP_CHECK(hipStreamSynchronize(Z.s));
+  TTS_REQUIRE(gc <= cap, "output capacity too small");
+  if (gc > 0)
+    HIP_CHECK(hipMemcpy(out_ids, st.out_ids + (size_t)slot * st.out_stride, (size_t)gc * 4, hipMemcpyDeviceToHost));
+  *n_out = gc;
+  *finished = Z.busy[slot] ? dn : 1;
+}
+
+void lm_slots_release(Engine* e, int slot) {
+  Engine::Slots& Z = e->slots;
+  TTS_REQUIRE(Z.open, "no slot batch open (tts_slots_open)");
+  TTS_REQUIRE(slot >= 0 && slot < Z.S, "slot out of range");
+  if (!Z.busy[slot]) return;
+  const StepState st = slots_state(e, Z.s);
+  int dn = 0;
+  HIP_CHECK(hipMemcpyAsync(&dn, st.done + slot, 4, hipMemcpyDeviceToHost, Z.s));
+  HIP_CHECK(hipStreamSynchronize(Z.s));
+  if (!dn) {  // aborted while running: stop the row and drop it from the active count
+    int act = 0;
+    const int one = 1;
+    HIP_CHECK(hipMemcpy(st.done + slot, &one, 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(&act, st.n_active, 4, hipMemcpyDeviceToHost));
+    --act;
+    HIP_CHECK(hipMemcpy(st.n_active, &act, 4, hipMemcpyHostToDevice));
+  }
+  Z.busy[slot] = 0;
 }
 
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,

@@ -36,6 +36,11 @@ EXPORTED_SYMBOLS = (
     "tts_generate_begin",
     "tts_generate_continue",
     "tts_generate_read",
+    "tts_slots_open",
+    "tts_slots_add",
+    "tts_slots_step",
+    "tts_slots_read",
+    "tts_slots_release",
     "tts_lm_score",
     "tts_lm_id_to_code",
     "tts_lm_last_timing",
@@ -152,6 +157,11 @@ def load_library() -> ctypes.CDLL:
         "tts_generate_begin": (I32, [P, ctypes.POINTER(GenParams), pi32, pi32, I32, P]),
         "tts_generate_continue": (I32, [P, I32, pi32]),
         "tts_generate_read": (I32, [P, pi32, I32, pi32]),
+        "tts_slots_open": (I32, [P, ctypes.POINTER(GenParams), I32, P]),
+        "tts_slots_add": (I32, [P, I32, pi32, I32, I32]),
+        "tts_slots_step": (I32, [P, I32, pi32]),
+        "tts_slots_read": (I32, [P, I32, pi32, I32, pi32, pi32]),
+        "tts_slots_release": (I32, [P, I32]),
         "tts_lm_score": (I32, [P, pi32, pi32, I32, I32, ctypes.POINTER(ctypes.c_float), P]),
         "tts_lm_id_to_code": (I32, [P, pi32, I32, pi32]),
         "tts_lm_last_timing": (I32, [P, ctypes.POINTER(F32), ctypes.POINTER(F32), pi32]),
