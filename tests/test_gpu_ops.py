@@ -63,7 +63,7 @@ def _tiled(lib, w, epi=0):
 
 
 @pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 40, 64])
-@pytest.mark.parametrize("N,K", [(256, 256), (3072, 2048), (2048, 8192)])
+@pytest.mark.parametrize("N,K", [(256, 256), (3072, 2048), (2048, 8192), (6144, 4096), (4096, 14336)])
 def test_wgemm_store(lib, M, N, K):
     g = torch.Generator().manual_seed(M * 7 + N)
     x = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16)
@@ -180,7 +180,7 @@ def test_wgemm_rows_independent(lib, M, N, K, epi):
 
 
 @pytest.mark.parametrize("M", [65, 202, 700])
-@pytest.mark.parametrize("N,K", [(384, 256), (3072, 2048), (2048, 8192)])
+@pytest.mark.parametrize("N,K", [(384, 256), (3072, 2048), (2048, 8192), (4096, 14336)])
 def test_pgemm_store_and_rows_independent(lib, M, N, K):
     """Prefill GEMM (tiles of the decode stream-plan layout, LDS-staged MFMA blocks) against
     the oracle's bf16 nn.Linear; the first and last rows are copies, so they must agree bit
@@ -195,7 +195,11 @@ def test_pgemm_store_and_rows_independent(lib, M, N, K):
     _check(lib.tts_op_pgemm(x.cuda().data_ptr(), M, K, wt.data_ptr(), N, out.data_ptr(), N, None, 0, None))
     torch.cuda.synchronize()
     o = out.cpu()
-    _bf16_close(o, ref)
+    if K > 8192:  # long sums: cancelled outputs carry more than 2 ulps of their own size
+        err = (o.float() - ref.float()).abs()
+        assert bool((err <= 2 * 2.0 ** -7 * ref.float().abs() + 2e-3).all())
+    else:
+        _bf16_close(o, ref)
     assert torch.equal(o[0], o[-1])
 
 

@@ -308,6 +308,10 @@ struct Ctx {
     for (int r0 = 0; r0 < rows; r0 += chunk) {
       const int m = std::min(chunk, rows - r0);
       WgemmPlan p = plan_wgemm(m, N, K, epi, e->num_cu);
+      if (p.sliced && wgemm_part_elems(p, m, ldo) * 4 > w.kpart.bytes) {
+        p.sliced = false;  // wide outputs (teacher-forced scoring over the vocabulary):
+        p.a_lds = false;   // A rows from global memory instead of fp32 chunk partials
+      }
       const bf16_t* xin = x ? x + (size_t)r0 * K : nullptr;
       bool norm = normw != nullptr;
       // fused RMSNorm only where the rows sit in registers (<= 16 rows, the early prologue):
@@ -335,10 +339,7 @@ struct Ctx {
       a.normw = normw; a.eps = c.rms_norm_eps;
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
-      if (p.sliced) {
-        TTS_REQUIRE(wgemm_part_elems(p, m, ldo) * 4 <= w.kpart.bytes, "K-sliced partial workspace too small");
-        a.part_out = w.kpart.as<float>();
-      }
+      if (p.sliced) a.part_out = w.kpart.as<float>();
       launch_wgemm(a, p, epi, norm, s);
     }
   }

@@ -94,7 +94,11 @@ TINY = LmArch("tiny", 256, 2, 4, 1, 64, 512, 2048, True)
 SMALL = LmArch("small", 512, 4, 8, 2, 64, 1536, 8192, True)
 TINY128 = LmArch("tiny128", 512, 2, 4, 1, 128, 1024, 2048, False, rope_factor=8.0)
 
-LM_ARCHS = {a.name: a for a in (TTS1, TTS1_MAX, TINY, SMALL, TINY128)}
+# TTS-1-Max dims with 2 layers: every kernel shape of config 4 (hd 128, K 4096 / 14336 in
+# K-chunked layouts, untied 193,856-row lm_head) at a size a CPU oracle checks in seconds.
+TTS1_MAX_2L = LmArch("tts1-max-2l", 4096, 2, 32, 8, 128, 14336, 193856, False, rope_factor=8.0)
+
+LM_ARCHS = {a.name: a for a in (TTS1, TTS1_MAX, TINY, SMALL, TINY128, TTS1_MAX_2L)}
 
 
 @dataclasses.dataclass(frozen=True)
