@@ -285,8 +285,15 @@ struct Ctx {
   int QKV() const { return M.qkv_n(); }
 
   // out = epi(x . W^T) over M rows (chunked by 64), RMSNorm prologue if normw != nullptr.
+  // w.xn holds RMSNorm(w.x, pending_norm) when a residual combine produced it (17..32-row
+  // decode: the down projection's K-sliced combine normalises with the next norm weight)
+  const bf16_t* pending_norm = nullptr;
+
   void gemm(const bf16_t* x, int rows, int K, const bf16_t* W, int N, const bf16_t* normw,
-            bf16_t* out, int ldo, bf16_t* resid, int epi, const WgemmArgs* logit_extra = nullptr) {
+            bf16_t* out, int ldo, bf16_t* resid, int epi, const WgemmArgs* logit_extra = nullptr,
+            const bf16_t* next_norm = nullptr) {
+    const bf16_t* ready = pending_norm;
+    if (resid) pending_norm = nullptr;  // the residual stream changes below
     if (rows > kPrefillChunk && x && pgemm_supported(rows, N, K, epi)) {
       // prefill: every prompt row of the batch in one LDS-staged MFMA launch
       const bf16_t* xin = x;
@@ -316,8 +323,12 @@ struct Ctx {
       bool norm = normw != nullptr;
       // fused RMSNorm only where the rows sit in registers (<= 16 rows, the early prologue):
       // at 17..64 rows every workgroup would normalise every row again — one standalone
-      // pass (same canonical order: identical bits) is cheaper
-      if (norm && (!p.a_lds || p.sliced || K > 4096 || m > 16)) {
+      // pass (same canonical order: identical bits) is cheaper, or none when the producer
+      // already wrote the normalised rows
+      if (norm && m > 16 && normw == ready && x == w.x.as<bf16_t>()) {
+        xin = w.xn.as<bf16_t>() + (size_t)r0 * K;
+        norm = false;
+      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || m > 16)) {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
@@ -340,7 +351,13 @@ struct Ctx {
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
       if (p.sliced) a.part_out = w.kpart.as<float>();
+      const bool fuse_norm = p.sliced && epi == EPI_RESID && next_norm && m > 16 && rows <= 32;
+      if (fuse_norm) {
+        a.next_norm = next_norm;
+        a.norm_out = w.xn.as<bf16_t>() + (size_t)r0 * ldo;
+      }
       launch_wgemm(a, p, epi, norm, s);
+      if (fuse_norm) pending_norm = next_norm;
     }
   }
 
@@ -366,6 +383,7 @@ struct Ctx {
 
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
+    pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
@@ -398,8 +416,9 @@ struct Ctx {
       }
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
+      const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
       gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),
-           EPI_RESID);
+           EPI_RESID, nullptr, decode ? next_norm : nullptr);
     }
   }
 

@@ -159,8 +159,12 @@ void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p, int epi, bool norm,
     const int Kfull = a.K;
     a.K = Kfull / p.sp.kc;  // the kernel's A chunk; ldx stays the full row
     launch_wgemm_store(a, p, false, s);
-    launch_splitk_combine(a.part_out, p.sp.kc, a.M, a.N, a.ldo, a.out, epi == EPI_RESID ? a.resid : nullptr,
-                          a.ldo, s);
+    if (epi == EPI_RESID && a.next_norm && a.norm_out)
+      launch_splitk_combine_norm(a.part_out, p.sp.kc, a.M, a.N, a.ldo, a.resid, a.ldo, a.next_norm, a.eps,
+                                 a.norm_out, a.ldo, s);
+    else
+      launch_splitk_combine(a.part_out, p.sp.kc, a.M, a.N, a.ldo, a.out, epi == EPI_RESID ? a.resid : nullptr,
+                            a.ldo, s);
     return;
   }
   a.part_out = nullptr;

@@ -72,6 +72,8 @@ struct WgemmArgs {
   int kc = 1;         // layout: K chunks (StreamPlan::kc, filled in by launch_wgemm)
   int sliced = 0;     // 1: grid.y = K chunk, K = one chunk, ldx = full K (filled in by launch_wgemm)
   float* part_out = nullptr;  // K-sliced launches: fp32 partials [kc][M][ldo] (caller's workspace)
+  const bf16_t* next_norm = nullptr;  // K-sliced residual launches: RMSNorm the updated rows
+  bf16_t* norm_out = nullptr;         //   with next_norm (eps) into norm_out [M][ldo]
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
 };
 
@@ -126,6 +128,9 @@ void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s);
 // K-sliced GEMM combine: v = bf16(sum_c part[c][m][n]);  resid ? resid += v : out = v
 void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
                            bf16_t* resid, int ldo, hipStream_t s);
+// residual combine + the next RMSNorm of the updated rows into xn (N % 8 == 0, N <= 32768)
+void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp, bf16_t* resid, int ldo,
+                                const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s);
 
 // ---- attention (lm_attn.hip)
 struct AttnArgs {

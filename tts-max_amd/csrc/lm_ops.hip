@@ -196,6 +196,66 @@ __global__ void splitk_combine_kernel(const float* __restrict__ part, int kc, in
   }
 }
 
+// The same combine for a residual epilogue, one workgroup per row, followed by the NEXT
+// RMSNorm of the updated row (LlamaRMSNorm, canonical sum order of chunk_sumsq): writes the
+// residual stream and its normalised copy, so the consumer GEMM stages plain rows.
+__global__ __launch_bounds__(256) void splitk_combine_norm_kernel(
+    const float* __restrict__ part, int kc, int M, int N, int ldp, bf16_t* __restrict__ resid, int ldo,
+    const bf16_t* __restrict__ normw, float eps, bf16_t* __restrict__ xn, int ldn) {
+  __shared__ float segs[64];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nchunk = N / 8;  // 8-column chunks; wave w takes 512-value segments w, w + 4, ...
+  bf16_t* r = resid + (size_t)m * ldo;
+  for (int base = wave * 64; base < nchunk; base += 256) {  // wave-uniform: full DPP rows
+    const int c = base + lane;
+    float s = 0.f;
+    if (c < nchunk) {
+    const int n = c * 8;
+    float v[8];
+    {
+      const float4* p = (const float4*)(part + (size_t)m * ldp + n);
+      const float4 a = p[0], b = p[1];
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    for (int k = 1; k < kc; ++k) {
+      const float4* p = (const float4*)(part + ((size_t)k * M + m) * ldp + n);
+      const float4 a = p[0], b = p[1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    const u32x4_t old = *(const u32x4_t*)(r + n);
+    u32x4_t pk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      pk[q] = pack_bf2(bf_lo(old[q]) + rbf(v[2 * q]), bf_hi(old[q]) + rbf(v[2 * q + 1]));
+    *(u32x4_t*)(r + n) = pk;
+    s = chunk_sumsq(pk);
+    }
+    s = wave_sum_dpp(s);
+    if (lane == 0) segs[base >> 6] = s;
+  }
+  __syncthreads();
+  float ss = 0.f;
+  for (int sg = 0; sg < (nchunk + 63) / 64; ++sg) ss += segs[sg];
+  const float rs = 1.0f / sqrtf(ss / (float)N + eps);
+  for (int base = wave * 64; base < nchunk; base += 256) {  // the chunks this thread wrote
+    const int c = base + lane;
+    if (c >= nchunk) break;
+    const int n = c * 8;
+    u32x4_t v = *(const u32x4_t*)(r + n);
+    const u32x4_t g = *(const u32x4_t*)(normw + n);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * rs)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * rs)));
+    *(u32x4_t*)(xn + (size_t)m * ldn + n) = v;
+  }
+}
+
+void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp, bf16_t* resid, int ldo,
+                                const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s) {
+  hipLaunchKernelGGL(splitk_combine_norm_kernel, dim3(M), dim3(256), 0, s, part, kc, M, N, ldp, resid, ldo,
+                     normw, eps, xn, ldn);
+}
+
 void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
                            bf16_t* resid, int ldo, hipStream_t s) {
   const int n = M * (N / 8);
