@@ -249,6 +249,43 @@ def test_rows_stop_at_different_steps():
     assert len({len(x) for x in batch}) > 1 or len(batch) == 1
 
 
+_FUSED_CHILD = r'''
+import json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
+from tts_amd import configs, synth
+from tts_amd.speechlm import MI355XSpeechLM
+arch = configs.TTS1
+m = MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=1, max_seq_len=1408)
+vocab = configs.vocab_for(arch)
+p = synth.synthetic_prompt(vocab, 3, 39, 150)
+new = m.generate_batch([p], max_length=1400, min_new_tokens=1400 - len(p), eos_token_id=-1, repetition_penalty=1.1)[0]
+print(json.dumps(new))
+'''
+
+
+def test_fused_qkv_attention_equals_separate_launches():
+    """The one-row decode step's QKV launch with the attention fused in (q/k/v handed to
+    appended attention workgroups as tagged granules, lm_gemm_kernel.h fattn_consumer) and
+    the separate chunked attention launch (TTS_FUSED_ATTN=0) produce the same greedy ids on
+    TTS-1 over 1.2k generated positions: 11 chunks of 128, so workgroups of the fused launch
+    also take a second chunk (chunk slots 0..2 of 8) and the new position crosses every
+    chunk boundary."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for v in ("1", "0"):
+        env = dict(os.environ, TTS_FUSED_ATTN=v)
+        r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, root], env=env, capture_output=True, text=True,
+                           timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[v] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(outs["1"]) == 1400 - 202
+    assert outs["1"] == outs["0"]
+
+
 @pytest.mark.parametrize("rows", [1, 8])
 def test_tts1_max_dims_logits_vs_oracle(rows):
     """BASELINE config 4's kernel shapes (TTS-1-Max: d 4096, hd 128, ffn 14336 in K-chunked

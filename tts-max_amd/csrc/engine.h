@@ -83,6 +83,7 @@ struct LmWork {
   DevBuf kv;           // [L][2][slots][KVH][max_seq][D]
   DevBuf x, xn, qkv, attn_out, act, q_rot, last_x;  // activations
   DevBuf part_o, part_ml;                           // attention split partials
+  DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]

@@ -15,6 +15,7 @@
 // sequence are merged later (o_proj prologue or attn_combine_kernel).
 #include "hip_common.h"
 #include "lm_kernels.h"
+#include "lm_attn_chunk.h"
 
 namespace tts {
 
@@ -105,62 +106,13 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
   }
   __syncthreads();
 
-  // 4. scores: wave = q head, lane = position
+  // 4-6. scores (lane = position), chunk softmax statistics, P.V (lane = dimension)
   const int g = wave;
-  const float* qg = qs + g * D;
-  float sc[PPL];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {
-    const int tl = lane + 64 * j;
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const u32x4_t kv = *(const u32x4_t*)(Ks + tl * KROW + c * 8);
-      const float4 q0 = *(const float4*)(qg + c * 8);
-      const float4 q1 = *(const float4*)(qg + c * 8 + 4);
-      acc += q0.x * bf_lo(kv[0]) + q0.y * bf_hi(kv[0]) + q0.z * bf_lo(kv[1]) + q0.w * bf_hi(kv[1]) +
-             q1.x * bf_lo(kv[2]) + q1.y * bf_hi(kv[2]) + q1.z * bf_lo(kv[3]) + q1.w * bf_hi(kv[3]);
-    }
-    sc[j] = (tl < n) ? acc * a.scale : -INFINITY;
-    mx = fmaxf(mx, sc[j]);
-  }
-  // 5. chunk softmax statistics (flash numerics: bf16 P for P.V, fp32 normaliser)
-  const float m = wave_max_dpp(mx);
-  float lsum = 0.f;
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {
-    const float p = (lane + 64 * j < n) ? expf(sc[j] - m) : 0.f;
-    lsum += p;
-    ps[g * SPLIT + lane + 64 * j] = rbf(p);
-  }
-  const float l = wave_sum_dpp(lsum);
+  float m, l;
+  attn_chunk_softmax<D, SPLIT>(Ks, qs + g * D, n, a.scale, lane, ps + g * SPLIT, m, l);
   __syncthreads();
-
-  // 6. P.V: wave = q head, lane = head dimension(s)
-  float o[DPL];
-#pragma unroll
-  for (int e = 0; e < DPL; ++e) o[e] = 0.f;
-  const float* pg = ps + g * SPLIT;
-#pragma unroll 8
-  for (int tl = 0; tl < n; ++tl) {
-    const float p = pg[tl];
-    if constexpr (DPL == 1) {
-      o[0] += p * bf2f(Vs[tl * KROW + lane]);
-    } else {
-      const uint32_t v2 = *(const uint32_t*)(Vs + tl * KROW + 2 * lane);
-      o[0] += p * bf_lo(v2);
-      o[1] += p * bf_hi(v2);
-    }
-  }
-  const int h = kvh * G + g;
-  const size_t pidx = ((size_t)row * a.H + h) * a.nsplit + sp;
-#pragma unroll
-  for (int e = 0; e < DPL; ++e) a.part_o[pidx * D + lane * DPL + e] = o[e];
-  if (lane == 0) {
-    a.part_ml[pidx * 2] = m;
-    a.part_ml[pidx * 2 + 1] = l;
-  }
+  const size_t pidx = ((size_t)row * a.H + kvh * G + g) * a.nsplit + sp;
+  attn_chunk_pv_store<D, SPLIT>(Vs, ps + g * SPLIT, n, lane, m, l, a.part_o + pidx * D, a.part_ml + pidx * 2);
 }
 
 int decode_split(int D) { return D == 64 ? 128 : 64; }

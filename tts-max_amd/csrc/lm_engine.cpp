@@ -244,6 +244,10 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
       std::max((size_t)R * w.nsplit_prefill, (size_t)B * w.nsplit_decode);
   w.part_o.alloc(part_rows * H * D * 4);
   w.part_ml.alloc(part_rows * H * 2 * 4);
+  w.gran.alloc((size_t)QKV / 2 * 8);
+  HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
+  w.ferr.alloc(256);
+  HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
   {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
     const int kmax = std::max(HID, std::max(FF, H * D));
     w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
@@ -271,6 +275,13 @@ namespace {
 // merges in LDS (TTS_ATTN_MERGED=1; measured 2x slower at batch 1: 8 CUs stream the KV).
 bool use_split_attn() {
   static const bool v = !(getenv("TTS_ATTN_MERGED") && atoi(getenv("TTS_ATTN_MERGED")));
+  return v;
+}
+
+// Decode attention of a one-row step fused into the QKV launch (lm_gemm_kernel.h,
+// fattn_consumer): default on; TTS_FUSED_ATTN=0 keeps the separate attention launch.
+bool use_fused_attn() {
+  static const bool v = !(getenv("TTS_FUSED_ATTN") && !atoi(getenv("TTS_FUSED_ATTN")));
   return v;
 }
 
@@ -381,22 +392,49 @@ struct Ctx {
     return a;
   }
 
+  // The one-row decode step's QKV launch carries the attention (TTS-1 geometry: head dim 64,
+  // decode chunks of 128 positions); consecutive fused launches differ in (pos, layer)
+  bool fused_attn_ok(int rows, bool decode) const {
+    return decode && rows == 1 && use_fused_attn() && use_split_attn() && c.head_dim == 64 &&
+           w.split_decode == 128 && c.num_layers >= 2 && c.num_layers <= 64 &&
+           wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu) &&
+           plan_wgemm(1, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu).a_lds;
+  }
+  WgemmArgs fused_attn_args(const AttnArgs& a, int layer) {
+    WgemmArgs fx;
+    fx.gran = w.gran.as<uint64_t>();
+    fx.fa = a;
+    fx.fattn_wgs = a.rows * a.KVH * std::min(8, a.nsplit);
+    fx.fattn_layer = layer;
+    fx.fattn_err = w.ferr.as<int>();
+    return fx;
+  }
+
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
+    const bool fattn = fused_attn_ok(rows, decode);
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
-      gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(),
-           nullptr, EPI_STORE);
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
-      // decode: one workgroup per (row, kv head) attends and merges (default), or the
-      // chunked kernel whose partials the o_proj prologue merges (TTS_ATTN_SPLIT=1)
+      if (fattn) {
+        const WgemmArgs fx = fused_attn_args(a, l);
+        gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
+             EPI_STORE, &fx);
+      } else {
+        gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
+             EPI_STORE);
+      }
+      // decode: the chunked kernel whose partials the o_proj prologue merges (default), or one
+      // workgroup per (row, kv head) that attends and merges (TTS_ATTN_MERGED=1)
       const bool split_attn = use_split_attn();
       // (rows <= 16: the merge scratch + A rows fit LDS beside the split-K partials)
       const bool fuse_combine = decode && split_attn && rows <= 16 &&
                                 plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
-      if (decode && !split_attn) {
+      if (fattn) {
+        // (attention ran inside the QKV launch)
+      } else if (decode && !split_attn) {
         launch_attn_decode_merged(a, s);
       } else if (decode) {
         launch_attn_decode_step(a, s);
@@ -671,6 +709,20 @@ int lm_gen_continue(Engine* e, int n_steps) {
   return G.finished ? 1 : 0;
 }
 
+// A fused QKV+attention launch whose granule wait timed out leaves garbage attention:
+// fail loudly at the next read (the flag is cleared for the next generation).
+static void check_fattn(Engine* e, hipStream_t s) {
+  if (!e->w.ferr.p) return;
+  int err = 0;
+  HIP_CHECK(hipMemcpyAsync(&err, e->w.ferr.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (err) {
+    HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 4, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    TTS_REQUIRE(false, "fused QKV+attention: a granule wait timed out (results invalid)");
+  }
+}
+
 void lm_gen_read(Engine* e, int32_t* out_ids, int out_stride, int32_t* out_lens) {
   Engine::Gen& G = e->gen;
   TTS_REQUIRE(G.open, "no generation in progress (tts_generate_begin)");
@@ -679,6 +731,7 @@ void lm_gen_read(Engine* e, int32_t* out_ids, int out_stride, int32_t* out_lens)
   std::vector<int> gc(G.B);
   HIP_CHECK(hipMemcpyAsync(gc.data(), st.gen_count, G.B * 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  check_fattn(e, s);
   for (int b = 0; b < G.B; ++b) {
     TTS_REQUIRE(gc[b] <= out_stride, "out_stride too small");
     out_lens[b] = gc[b];
@@ -814,6 +867,7 @@ int lm_slots_step(Engine* e, int n_steps) {
   TTS_REQUIRE(Z.open, "no slot batch open (tts_slots_open)");
   const StepState st = slots_state(e, Z.s);
   for (int n = 0; n < n_steps; ++n) HIP_CHECK(hipGraphLaunch(e->w.graph, Z.s));
+  check_fattn(e, Z.s);
   int act = 0;
   HIP_CHECK(hipMemcpyAsync(&act, st.n_active, 4, hipMemcpyDeviceToHost, Z.s));
   HIP_CHECK(hipStreamSynchronize(Z.s));
@@ -861,7 +915,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 5 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which >= 0 && which <= 6 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which != 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
   hipStream_t s = e->stream;
   Ctx X(e, s);
   const tts_lm_config& c = X.c;
@@ -900,7 +955,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   // not still cached from the previous launch: the timing reflects HBM streaming
   int it_layer = 0;
   auto launch = [&]() {
-    const LmLayer& ly = X.M.layers[it_layer++ % c.num_layers];
+    const int li = it_layer++ % c.num_layers;
+    const LmLayer& ly = X.M.layers[li];
     switch (which) {
       case 0:
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr, EPI_STORE);
@@ -933,6 +989,15 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         else launch_attn_decode_merged(aa, s);
         b = (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2 + act_rw * QKV;
         break;
+      case 6: {  // QKV with the decode attention fused in (the one-row decode step's form)
+        const AttnArgs al = X.attn_args(li, rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
+        const WgemmArgs fx = X.fused_attn_args(al, li);
+        X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr,
+               EPI_STORE, &fx);
+        b = 2.0 * QKV * HID + act_rw * (HID + QKV) + 2.0 * HID +
+            (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2;
+        break;
+      }
     }
   };
   launch();
@@ -945,6 +1010,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   HIP_CHECK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
   *avg_ms = ms / iters;
   *bytes = b;
+  check_fattn(e, s);
 }
 
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,

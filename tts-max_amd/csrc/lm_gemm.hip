@@ -139,6 +139,16 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   return p;
 }
 
+// The one-row QKV launch can carry the fused decode attention (fattn_consumer) when it takes
+// the register-staged RMSNorm prologue (the EARLY instantiation, as launch_one decides).
+bool wgemm_fattn_ok(int N, int K, int num_cu) {
+  const WgemmPlan p = plan_wgemm(1, N, K, EPI_STORE, num_cu);
+  if (!p.a_lds || p.sliced || K > 4096) return false;
+  const int kch = K / 8, NT = p.sp.waves * 64;
+  const int ea = p.sp.waves >= 16 ? 1 : (p.sp.waves >= 8 ? 2 : 4);  // wgemm_ea
+  return kch % 64 == 0 && (kch + NT - 1) / NT <= ea;
+}
+
 bool wgemm_supported(int M, int N, int K, int epi) {
   const int NG = (epi == EPI_SWIGLU) ? 2 : 1;
   return M >= 1 && M <= 64 && (N % (16 * NG)) == 0 && (K % 256) == 0;

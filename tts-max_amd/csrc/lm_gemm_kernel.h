@@ -8,6 +8,7 @@
 
 #include "hip_common.h"
 #include "lm_kernels.h"
+#include "lm_attn_chunk.h"
 
 namespace tts {
 
@@ -33,6 +34,129 @@ inline bool wgemm_attn_early(int M, int K, int nsplit, int waves) {
   return (nsplit + groups - 1) / groups <= wgemm_cpg(waves);
 }
 
+// ------------------------------------------------- attention fused into the QKV launch -----
+// One appended workgroup = one (row, kv head, chunk slot c0); it attends chunks c0,
+// c0 + nslot, ... of SPLIT positions.  Its first chunk's K/V rows are loaded at entry, while
+// the projection workgroups still stream the QKV weights; then threads poll the granules of
+// the group's q (and, in the workgroup holding the new position, k and v) until their tag
+// is this launch's, and the chunk math runs exactly as in attn_decode2 (lm_attn_chunk.h).
+constexpr int FATTN_D = 64, FATTN_SPLIT = 128, FATTN_G = 4;
+constexpr size_t fattn_lds_bytes() {
+  return (size_t)2 * FATTN_SPLIT * (FATTN_D + 8) * 2 + FATTN_G * FATTN_D * 4 + FATTN_G * FATTN_SPLIT * 4 +
+         (FATTN_G * FATTN_D / 2 + FATTN_D) * 4 + FATTN_D * 2;
+}
+constexpr int FATTN_MAX_SPINS = 1 << 16;  // ~0.1 s: the wait always ends (fattn_err set)
+
+template <int NT>
+TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
+  constexpr int D = FATTN_D, SPLIT = FATTN_SPLIT, G = FATTN_G;
+  constexpr int KROW = D + 8, CH = D / 8, H2 = D / 2;
+  constexpr int LOADS = (SPLIT * CH + NT - 1) / NT;
+  const AttnArgs& a = wa.fa;
+  bf16_t* Ks = (bf16_t*)smem;
+  bf16_t* Vs = Ks + SPLIT * KROW;
+  float* qs = (float*)(Vs + SPLIT * KROW);
+  float* ps = qs + G * D;
+  uint32_t* raw = (uint32_t*)(ps + G * SPLIT);  // q pairs [G*D/2] | k pairs [D/2] | v pairs [D/2]
+  const bf16_t* rawb = (const bf16_t*)raw;
+  bf16_t* knew = (bf16_t*)(raw + G * D / 2 + D);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrk = a.rows * a.KVH;
+  const int nslot = wa.fattn_wgs / nrk;
+  const int rk = b % nrk, c0 = b / nrk;
+  const int row = rk / a.KVH, kvh = rk % a.KVH;
+  const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
+  if (c0 * SPLIT >= ctx) return;  // (whole workgroup, before any barrier)
+  const bool has_new = ((pos / SPLIT) - c0) % nslot == 0;
+  const size_t cbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
+  const bf16_t* kc = a.kcache + cbase;
+  const bf16_t* vc = a.vcache + cbase;
+
+  u32x4_t kr4[LOADS], vr4[LOADS];
+  auto load_chunk = [&](int sp) {
+    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx);
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {  // unconditional (clamped row)
+      const int q = min(tid + i * NT, SPLIT * CH - 1), tl = q / CH, c = q % CH;
+      const int t = (t0 + tl < t1) ? t0 + tl : t0;
+      kr4[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
+      vr4[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
+    }
+  };
+  load_chunk(c0);
+  const int qi = min(tid, G * D - 1), qd = qi % D;
+  const float qc = bf2f(a.rope_cos[(size_t)pos * D + qd]), qsn = bf2f(a.rope_sin[(size_t)pos * D + qd]);
+
+  auto stage_chunk = [&](int sp) {  // registers -> LDS tiles (the new position excluded)
+    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx);
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int q = tid + i * NT, tl = q / CH, c = q % CH, t = t0 + tl;
+      if (q < SPLIT * CH && t < t1 && t != pos) {
+        *(u32x4_t*)(Ks + tl * KROW + c * 8) = kr4[i];
+        *(u32x4_t*)(Vs + tl * KROW + c * 8) = vr4[i];
+      }
+    }
+  };
+  stage_chunk(c0);  // before the wait: only q-dependent work remains after it
+
+  // wait for the projection's granules of this kv group
+  const uint32_t tag = ((uint32_t)pos << 6) | (uint32_t)wa.fattn_layer;
+  const int nq = G * D / 2, ngr = has_new ? nq + D : nq;
+  if (tid < ngr) {
+    int col;
+    if (tid < nq) col = kvh * G * D + 2 * tid;
+    else if (tid < nq + D / 2) col = a.H * D + kvh * D + 2 * (tid - nq);
+    else col = a.H * D + a.KVH * D + kvh * D + 2 * (tid - nq - D / 2);
+    const uint64_t* gp = wa.gran + (size_t)row * (a.ld_qkv / 2) + col / 2;
+    uint64_t v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while ((uint32_t)(v >> 32) != tag) {
+      if (++spins > FATTN_MAX_SPINS) {
+        __hip_atomic_store(wa.fattn_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    raw[tid] = (uint32_t)v;
+  }
+  __syncthreads();
+  // RoPE of the group's q heads; the new position's roped k and v to the cache
+  if (tid < G * D) {
+    const int g = tid / D;
+    qs[tid] = rope_elem(rawb[tid], rawb[g * D + (qd < H2 ? qd + H2 : qd - H2)], qd < H2, qc, qsn);
+  }
+  if (has_new && tid < D) {
+    const bf16_t kb = f2bf(rope_elem(rawb[G * D + tid], rawb[G * D + (tid < H2 ? tid + H2 : tid - H2)],
+                                     tid < H2, qc, qsn));
+    knew[tid] = kb;
+    a.kcache[cbase + (size_t)pos * D + tid] = kb;
+    a.vcache[cbase + (size_t)pos * D + tid] = rawb[G * D + D + tid];
+  }
+  for (int sp = c0; sp * SPLIT < ctx; sp += nslot) {
+    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx), n = t1 - t0;
+    if (sp != c0) {
+      __syncthreads();  // the previous chunk's readers are done
+      stage_chunk(sp);
+    }
+    if (pos >= t0 && pos < t1 && tid < D) {
+      Ks[(pos - t0) * KROW + tid] = knew[tid];
+      Vs[(pos - t0) * KROW + tid] = rawb[G * D + D + tid];
+    }
+    __syncthreads();  // tiles, qs visible
+    if ((sp + nslot) * SPLIT < ctx) load_chunk(sp + nslot);  // next chunk in flight
+    if (wave < G) {
+      float m, l;
+      attn_chunk_softmax<D, SPLIT>(Ks, qs + wave * D, n, a.scale, lane, ps + wave * SPLIT, m, l);
+      const size_t pidx = ((size_t)row * a.H + kvh * G + wave) * a.nsplit + sp;
+      attn_chunk_pv_store<D, SPLIT>(Vs, ps + wave * SPLIT, n, lane, m, l, a.part_o + pidx * D,
+                                    a.part_ml + pidx * 2);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- the GEMM kernel -----
 // One workgroup = WAVES waves; KSPLIT consecutive waves split the K range of one unit
 // (a unit = NG n-tiles of 16 output columns), WAVES/KSPLIT units run side by side, and
@@ -55,6 +179,13 @@ template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM
 __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
+  constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && NORM && EARLY;
+  if constexpr (FATT) {
+    if (a.fattn_wgs && (int)blockIdx.x >= (int)gridDim.x - a.fattn_wgs) {
+      fattn_consumer<NT>(a, smem, blockIdx.x - (gridDim.x - a.fattn_wgs));
+      return;
+    }
+  }
   constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -75,7 +206,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   const int kt_base = a.sliced ? blockIdx.y * KTc : 0;      // first k-tile held in A
   const bf16_t* xg = a.x ? a.x + (a.sliced ? (size_t)blockIdx.y * a.K : 0) : nullptr;
   const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
-  const int ustride = gridDim.x * UPW;
+  const int ustride = (gridDim.x - a.fattn_wgs) * UPW;  // (appended attention workgroups excluded)
 
   bf16_t* xs = (bf16_t*)smem;
   const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
@@ -174,6 +305,11 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         seen_cur[mt][r] = a.seen[(size_t)m * a.seen_stride + (u_first >> 1)];
       }
     }
+
+  uint32_t ftag = 0;  // fused attention: this launch's granule tag (row 0)
+  if constexpr (FATT) {
+    if (a.fattn_wgs) ftag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
+  }
 
   // ---- then the weight stream
   // stage st of the wave's item of unit uu: NG*KU consecutive tiles (StreamPlan layout)
@@ -569,6 +705,17 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
     }
+    if constexpr (FATT) {  // publish the unit's 16 columns of row 0 as 8 granules
+      if (kpart == 0 && active && a.fattn_wgs) {
+        const uint32_t mine = (uint32_t)f2bf(acc[0][0][0]);
+        const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+        if (lane < 16 && !(lane & 1)) {
+          const int n = u * 16 + lane;
+          const uint64_t g = ((uint64_t)ftag << 32) | (other << 16) | mine;
+          __hip_atomic_store(a.gran + n / 2, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
     first = false;
     if constexpr (EPI == EPI_LOGITS) {
 #pragma unroll
@@ -637,6 +784,14 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   lds += (size_t)wgemm_red_floats(WAVES, KSPLIT, NG, mt, a.M, a.K) * sizeof(float);
   if (ASRC == A_ATTN)  // chunk factors (fallback path) or chunk-group partials (early path)
     lds += std::max((size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit, (size_t)WAVES * 64 * 8) * sizeof(float);
+  if (a.fattn_wgs) {  // QKV + fused decode attention (one row, D 64, chunks of 128)
+    if (!(EPI == EPI_STORE && ASRC == A_LDS && NORM && a.M == 1 && a.fa.D == FATTN_D &&
+          a.fa.split == FATTN_SPLIT && a.gran && a.fattn_err && !a.sliced))
+      throw std::runtime_error("wgemm: fused attention needs the one-row QKV launch (D 64, split 128)");
+    if (!EARLY) throw std::runtime_error("wgemm: fused attention needs the register-staged prologue");
+    lds = std::max(lds, fattn_lds_bytes());
+    grid += a.fattn_wgs;
+  }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
   const dim3 g(grid, a.sliced ? a.kc : 1);
   if (mt == 1)

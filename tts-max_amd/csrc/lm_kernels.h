@@ -40,6 +40,27 @@ __host__ __device__ inline long long plan_tile(int ng, int ksplit, int ku, int u
 StreamPlan stream_plan(int N, int K, int ng, int num_cu);
 constexpr int LOGITS_MAX_PARTS = 1024;  // lm_head workgroups = argmax partials per row
 
+struct AttnArgs {
+  const bf16_t* qkv = nullptr;  // [rows][ld_qkv]: q (H*D) | k (KVH*D) | v (KVH*D)
+  int ld_qkv = 0;
+  int rows = 0;
+  const int* row_slot = nullptr;  // KV slot (sequence) of each query row
+  const int* row_pos = nullptr;   // absolute position of each query row
+  bf16_t* kcache = nullptr;       // this layer: [slots][KVH][max_seq][D]
+  bf16_t* vcache = nullptr;
+  int max_seq = 0;
+  const bf16_t* rope_cos = nullptr;  // [max_seq][D]
+  const bf16_t* rope_sin = nullptr;
+  int H = 0, KVH = 0, D = 0;
+  float scale = 0.f;
+  int split = 0;      // positions per split-K chunk
+  int nsplit = 0;     // max chunks per row (grid.y)
+  float* part_o = nullptr;  // [rows][H][nsplit][D]
+  float* part_ml = nullptr; // [rows][H][nsplit][2] (running max, sum)
+  bf16_t* q_rot = nullptr;  // prefill: roped q [rows][H*D]
+  bf16_t* out = nullptr;    // [rows][H*D] bf16
+};
+
 struct WgemmArgs {
   const bf16_t* x = nullptr;  // A: [M][ldx] bf16 activations
   int M = 0, K = 0, ldx = 0;
@@ -74,6 +95,17 @@ struct WgemmArgs {
   float* part_out = nullptr;  // K-sliced launches: fp32 partials [kc][M][ldo] (caller's workspace)
   const bf16_t* next_norm = nullptr;  // K-sliced residual launches: RMSNorm the updated rows
   bf16_t* norm_out = nullptr;         //   with next_norm (eps) into norm_out [M][ldo]
+  // QKV launch with the decode attention fused in (decode, one row): the projection's
+  // workgroups publish q/k/v as data-tagged 8-byte granules {bf16 pair, tag} with
+  // agent-scope stores; fattn_wgs extra workgroups (blockIdx.x >= the GEMM grid) each load
+  // one K/V chunk, wait for their q (and the new k/v) granules and write the chunk
+  // partials exactly as attn_decode2 does.  tag = (pos << 6) | layer differs between any
+  // two consecutive launches, so a granule left by the previous launch never matches.
+  uint64_t* gran = nullptr;   // [M][ldo / 2]
+  AttnArgs fa;                // the attention of this layer (decode split, part_o / part_ml)
+  int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
+  int fattn_layer = 0;
+  int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
 };
 
@@ -98,6 +130,7 @@ inline size_t wgemm_part_elems(const WgemmPlan& p, int M, int ldo) {
   return p.sliced ? (size_t)p.sp.kc * M * ldo : 0;
 }
 bool wgemm_supported(int M, int N, int K, int epi);
+bool wgemm_fattn_ok(int N, int K, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
 
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
@@ -133,26 +166,6 @@ void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp
                                 const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s);
 
 // ---- attention (lm_attn.hip)
-struct AttnArgs {
-  const bf16_t* qkv = nullptr;  // [rows][ld_qkv]: q (H*D) | k (KVH*D) | v (KVH*D)
-  int ld_qkv = 0;
-  int rows = 0;
-  const int* row_slot = nullptr;  // KV slot (sequence) of each query row
-  const int* row_pos = nullptr;   // absolute position of each query row
-  bf16_t* kcache = nullptr;       // this layer: [slots][KVH][max_seq][D]
-  bf16_t* vcache = nullptr;
-  int max_seq = 0;
-  const bf16_t* rope_cos = nullptr;  // [max_seq][D]
-  const bf16_t* rope_sin = nullptr;
-  int H = 0, KVH = 0, D = 0;
-  float scale = 0.f;
-  int split = 0;      // positions per split-K chunk
-  int nsplit = 0;     // max chunks per row (grid.y)
-  float* part_o = nullptr;  // [rows][H][nsplit][D]
-  float* part_ml = nullptr; // [rows][H][nsplit][2] (running max, sum)
-  bf16_t* q_rot = nullptr;  // prefill: roped q [rows][H*D]
-  bf16_t* out = nullptr;    // [rows][H*D] bf16
-};
 void launch_rope_append(const AttnArgs& a, hipStream_t s);       // prefill: rope q,k; append k,v
 void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
 // decode step: register-streamed chunks of decode_split(D) positions, KV append fused

@@ -289,7 +289,8 @@ class MI355XSpeechLM:
     def bench_kernel(self, which: str, rows: int = 1, ctx: int = 450, iters: int = 50) -> tuple[float, float]:
         """(avg ms per launch, algorithmic bytes per launch) of one decode-step kernel."""
         ms, b = ctypes.c_float(), ctypes.c_double()
-        _lib.check(self._lib.tts_lm_bench_kernel(self._h, self.KERNELS.index(which), rows, ctx, iters,
+        sel = 6 if which == "qkv_attn" else self.KERNELS.index(which)  # qkv_attn: QKV + fused attention
+        _lib.check(self._lib.tts_lm_bench_kernel(self._h, sel, rows, ctx, iters,
                                                  ctypes.byref(ms), ctypes.byref(b)))
         return ms.value, b.value
 
