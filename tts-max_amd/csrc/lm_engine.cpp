@@ -397,8 +397,7 @@ struct Ctx {
   bool fused_attn_ok(int rows, bool decode) const {
     return decode && rows == 1 && use_fused_attn() && use_split_attn() && c.head_dim == 64 &&
            w.split_decode == 128 && c.num_layers >= 2 && c.num_layers <= 64 &&
-           wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu) &&
-           plan_wgemm(1, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu).a_lds;
+           wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
   }
   WgemmArgs fused_attn_args(const AttnArgs& a, int layer) {
     WgemmArgs fx;
@@ -431,7 +430,7 @@ struct Ctx {
       const bool split_attn = use_split_attn();
       // (rows <= 16: the merge scratch + A rows fit LDS beside the split-K partials)
       const bool fuse_combine = decode && split_attn && rows <= 16 &&
-                                plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
+                                wgemm_oproj_merge_ok(rows, HID, HD, w.nsplit_decode, e->num_cu);
       if (fattn) {
         // (attention ran inside the QKV launch)
       } else if (decode && !split_attn) {
@@ -945,7 +944,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   ex.part_stride = LOGITS_MAX_PARTS;
   // attention chunk partials for the fused o_proj prologue
   launch_attn_decode_step(aa, s);
-  const bool fuse_o = use_split_attn() && rows <= 16 && plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu).a_lds;
+  const bool fuse_o = use_split_attn() && rows <= 16 &&
+                      wgemm_oproj_merge_ok(rows, HID, HD, e->w.nsplit_decode, e->num_cu);
   WgemmArgs exo;
   exo.attn_o = aa.part_o; exo.attn_ml = aa.part_ml; exo.attn_pos = e->w.row_pos.as<int>();
   exo.attn_split = aa.split; exo.attn_nsplit = aa.nsplit; exo.attn_D = aa.D;

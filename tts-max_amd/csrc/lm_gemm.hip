@@ -131,6 +131,15 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   p.grid = p.sp.grid;
   const int w = p.sp.waves, ks = p.sp.ksplit;
   p.a_lds = wgemm_lds_bytes(w, ks, ng, M, K, true) <= kLdsBudget;
+  // Up to 16 rows, a residual projection whose rows do not fit the LDS prologue and whose
+  // K-sliced form would run the grid in more than two rounds (TTS-1-Max down, K 14336: 7
+  // chunks x 256 workgroups) streams its A fragments from L2 beside the weights (A_GLOBAL
+  // ring) instead: at 8 rows 39 -> 23 us.  (TTS-1 down at 16 rows, 4 chunks x 128: the
+  // sliced form is faster, 14.5 vs 15.5 us; at 17..32 rows the ring drops to one stage and
+  // loses.)  Unsliced also keeps these rows' sums in the batch-1 order.  TTS_AGR=0: off.
+  static const bool agr_on = !(getenv("TTS_AGR") && !atoi(getenv("TTS_AGR")));
+  if (agr_on && M <= 16 && epi == EPI_RESID && !p.a_lds && p.sp.kc > 1 && p.grid * p.sp.kc > 2 * num_cu)
+    return p;  // a_lds = false, unsliced
   if (!p.a_lds && p.sp.kc > 1 && (epi == EPI_STORE || epi == EPI_RESID) &&
       wgemm_lds_bytes(w, ks, ng, M, K / p.sp.kc, true) <= kLdsBudget) {
     p.a_lds = true;
@@ -147,6 +156,13 @@ bool wgemm_fattn_ok(int N, int K, int num_cu) {
   const int kch = K / 8, NT = p.sp.waves * 64;
   const int ea = p.sp.waves >= 16 ? 1 : (p.sp.waves >= 8 ? 2 : 4);  // wgemm_ea
   return kch % 64 == 0 && (kch + NT - 1) / NT <= ea;
+}
+
+// o_proj with the attention-chunk merge as its prologue (A_ATTN): only where the merge
+// takes the register-staged form; otherwise the merge kernel + a plain o_proj is faster.
+bool wgemm_oproj_merge_ok(int M, int N, int K, int nsplit, int num_cu) {
+  const WgemmPlan p = plan_wgemm(M, N, K, EPI_RESID, num_cu);
+  return p.a_lds && !p.sliced && wgemm_attn_early(M, K, nsplit, p.sp.waves);
 }
 
 bool wgemm_supported(int M, int N, int K, int epi) {

@@ -327,17 +327,35 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // the stage R positions later (next unit's stages once this unit's are all issued).
   const int S = a.sliced ? Sc : kc * Sc;  // stages per item in this launch
   u32x4_t wr[R][KU][NG];
+  // A_GLOBAL (rows that do not fit the LDS prologue): the A fragments of a stage ride in the
+  // ring beside its weight tiles (L2 hits, issued with the stage), so no MFMA waits on an
+  // L2 round trip; 1..2 m-tiles (MT_MAX 4 keeps the loads inside consume)
+  constexpr bool AGR = ASRC == A_GLOBAL && MT_MAX <= 2;
+  const int arow = lane & 15;
+  const int akoff = 8 * (lane >> 4);
+  u32x4_t ar[R][KU][AGR ? MT_MAX : 1];
   int pu = u, ps = 0;  // next stage to issue
   // The refills are issued only where the stage exists by construction (never behind a
   // per-iteration condition): every path then has a fixed load count and the compiler's
   // vmcnt waits stay exact (a conditional issue makes it merge paths pessimistically,
   // i.e. drain the ring at every stage).
-  auto issue = [&](u32x4_t (&dst)[KU][NG]) {
+  auto issue = [&](u32x4_t (&dst)[KU][NG], u32x4_t (&adst)[KU][AGR ? MT_MAX : 1]) {
     const u32x4_t* q = sptr(pu, ps);
 #pragma unroll
     for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
       for (int g = 0; g < NG; ++g) dst[kk][g] = __builtin_nontemporal_load(q + (g * KU + kk) * 64);
+    if constexpr (AGR) {
+      const int sg = ps + st_off, ch = kc == 1 ? 0 : sg / Sc;
+      const int kt = ch * KTc + kpart * kt_pc + (sg - ch * Sc) * KU - kt_base;
+#pragma unroll
+      for (int kk = 0; kk < KU; ++kk)
+#pragma unroll
+        for (int mt = 0; mt < MT_MAX; ++mt) {
+          const int m = min(mt * 16 + arow, M - 1);
+          adst[kk][mt] = *(const u32x4_t*)(xg + (size_t)m * a.ldx + (kt + kk) * 32 + akoff);
+        }
+    }
     if (++ps == S) { ps = 0; pu += ustride; }
   };
   // every wave's operand loads enter the CU's memory pipeline ahead of any weight load; the
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // (unconditional: a wave with no unit streams unit units-1, never consumed (sptr clamps).
   // A branch here would make every prologue wait below drain the primed stages as well)
 #pragma unroll
-  for (int j = 0; j < R; ++j) issue(wr[j]);
+  for (int j = 0; j < R; ++j) issue(wr[j], ar[j]);
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
@@ -569,8 +587,6 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
    }
   }
 
-  const int arow = lane & 15;
-  const int akoff = 8 * (lane >> 4);
 
   // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
   float best_v[MT_MAX][4];
@@ -601,7 +617,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
       for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    auto consume = [&](const u32x4_t (&src)[KU][NG], int stage) {
+    auto consume = [&](const u32x4_t (&src)[KU][NG], const u32x4_t (&asrc)[KU][AGR ? MT_MAX : 1], int stage) {
       const int sg = stage + st_off, ch = kc == 1 ? 0 : sg / Sc;
       const int kt = ch * KTc + kpart * kt_pc + (sg - ch * Sc) * KU - kt_base;  // A column tile
 #pragma unroll
@@ -611,7 +627,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         for (int mt = 0; mt < MT_MAX; ++mt) {  // (all MT_MAX tiles: no branch, exact vmcnt)
           const int m = min(mt * 16 + arow, M - 1);  // rows >= M: duplicates, never stored
           u32x4_t av;
-          if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
+          if constexpr (AGR) av = asrc[kk][mt];
+          else if constexpr (ASRC != A_GLOBAL) av = *(const u32x4_t*)(xs + (size_t)m * ldxs + k);
           else av = *(const u32x4_t*)(xg + (size_t)m * a.ldx + k);
           const bf16x8_t af = as_bf16x8(av);
 #pragma unroll
@@ -624,15 +641,15 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     if (u + ustride < units) {  // the wave has a next unit: every refill exists
       for (int st = 0; st < S; st += R) {
 #pragma unroll
-        for (int j = 0; j < R; ++j) { consume(wr[j], st + j); issue(wr[j]); }
+        for (int j = 0; j < R; ++j) { consume(wr[j], ar[j], st + j); issue(wr[j], ar[j]); }
       }
     } else {  // last unit of the wave (or none): refill while stages remain, then drain
       for (int st = 0; st + R < S; st += R) {
 #pragma unroll
-        for (int j = 0; j < R; ++j) { consume(wr[j], st + j); issue(wr[j]); }
+        for (int j = 0; j < R; ++j) { consume(wr[j], ar[j], st + j); issue(wr[j], ar[j]); }
       }
 #pragma unroll
-      for (int j = 0; j < R; ++j) consume(wr[j], S - R + j);
+      for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j);
     }
 
     if (a.diag & 2) {
@@ -824,7 +841,9 @@ template <int C, int NG, int ASRC, bool NORM, int EPI>
 static void launch_shape(const WgemmArgs& a, int grid, hipStream_t s) {
   constexpr Shape3 h = kShapes[C];
   const int S = (a.K / 32) / (h.ksplit * h.ku);  // (sliced: stages of one chunk)
-  if (h.r >= 2 && S % 2 == 0) launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 2>(a, grid, s);
+  // (A_GLOBAL rides A fragments in the ring: one stage deep where two would spill)
+  const bool agr_r1 = ASRC == A_GLOBAL && (h.ku >= 4 || a.M > 16);
+  if (h.r >= 2 && S % 2 == 0 && !agr_r1) launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 2>(a, grid, s);
   else launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 1>(a, grid, s);
 }
 

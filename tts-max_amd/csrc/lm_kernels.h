@@ -131,6 +131,7 @@ inline size_t wgemm_part_elems(const WgemmPlan& p, int M, int ldo) {
 }
 bool wgemm_supported(int M, int N, int K, int epi);
 bool wgemm_fattn_ok(int N, int K, int num_cu);
+bool wgemm_oproj_merge_ok(int M, int N, int K, int nsplit, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
 
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
