@@ -98,6 +98,10 @@ StreamPlan stream_plan(int N, int K, int ng, int num_cu) {
   // EPI_LOGITS hold at most LOGITS_MAX_PARTS workgroups
   const int cap = (fgrid > 0) ? std::min(fgrid, LOGITS_MAX_PARTS) : num_cu;
   p.grid = std::min(grid, cap);
+  // between one and two rounds of units per CU, a full grid leaves half the workgroups with
+  // one round more than the rest (TTS-1-Max qkv: 384 units on 256 CUs): balance the rounds
+  static const bool balance = !(getenv("TTS_BALANCE") && !atoi(getenv("TTS_BALANCE")));
+  if (balance && fgrid <= 0 && grid > num_cu && grid < 2 * num_cu) p.grid = (grid + 1) / 2;
   // K chunks of 2048 columns (64 k-tiles) where the shape divides them: at batch 17..32 one
   // chunk of A (32 x 2048 bf16 = 128 KiB) fits LDS where the whole K (8192) does not
   if (K > 2048 && K % 2048 == 0 && (2048 / 32) % (p.ksplit * p.ku) == 0) p.kc = K / 2048;
