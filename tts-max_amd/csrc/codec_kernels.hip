@@ -188,9 +188,177 @@ static void launch_split(GemmF32Args g, int target, hipStream_t s) {
                      g.M, g.N, g.bias, g.act, g.resid, g.C, g.ldc);
 }
 
+// ------------------------------------------------- fp32 GEMM as three bf16 MFMA products -----
+// The codec is fp32 end to end (the reference never casts).  fp32 MFMA (32x32x2) peaks at a
+// sixteenth of the bf16 rate on CDNA4, so every fp32 operand is split once, in the LDS staging,
+// into x = h + m + l with h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (24 significant
+// bits: the fp32 value), and a.b = ah.bh + (ah.bm + am.bh) + (ah.bl + al.bh + am.bm) with fp32
+// accumulation (v_mfma_f32_32x32x16_bf16, smallest terms first); the dropped terms are
+// <= 2^-24 relative, i.e. fp32 products.  Same tiles, staging order and epilogue as
+// gemm_f32_kernel.
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
+  constexpr int BK = 32, LS = BK + 8;           // bf16 row stride 80 B
+  constexpr int MI = TM / 64, NJ = TN / 64;     // 32x32 accumulators per wave
+  constexpr int TPA = 256 / TM, KPA = BK / TPA; // A staging: threads per row, floats per thread
+  constexpr int TPB = 256 / TN, KPB = BK / TPB;
+  __shared__ __attribute__((aligned(16))) bf16_t Ah[TM * LS], Am[TM * LS], Al[TM * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t Bh[TN * LS], Bm[TN * LS], Bl[TN * LS];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbn = (g.N + TN - 1) / TN;
+  const int m0 = (blockIdx.x / nbn) * TM, n0 = (blockIdx.x % nbn) * TN;
+  const int kbeg = blockIdx.y * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int arow = t / TPA, ak = (t % TPA) * KPA;
+  const int brow = t / TPB, bk = (t % TPB) * KPB;
+  const int ar = m0 + arow, br = n0 + brow;
+  const bool aok = ar < g.M, bok = br < g.N;
+  const float* ap = g.A + (size_t)(aok ? ar : g.M - 1) * g.lda + kbeg + ak;
+  const float* bp = g.B + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk;
+  f32x16_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ra[KPA / 4], rb[KPB / 4];
+  auto load = [&](int kn) {
+#pragma unroll
+    for (int v = 0; v < KPA / 4; ++v) {
+      const float4 l = *(const float4*)(ap + kn + 4 * v);
+      ra[v] = aok ? l : z4;
+    }
+#pragma unroll
+    for (int v = 0; v < KPB / 4; ++v) {
+      const float4 l = *(const float4*)(bp + kn + 4 * v);
+      rb[v] = bok ? l : z4;
+    }
+  };
+  // 8 fp32 -> 8 bf16 each of h, m, l (exact residuals: x - h and x - h - m are fp32-exact),
+  // one 16-B store per plane
+  auto split8 = [](const float4& x0, const float4& x1, bf16_t* hp, bf16_t* mp, bf16_t* lp) {
+    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    u32x4_t h, m, l;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float h0 = rbf(v[2 * q]), h1 = rbf(v[2 * q + 1]);
+      const float r0 = v[2 * q] - h0, r1 = v[2 * q + 1] - h1;
+      const float m0 = rbf(r0), m1 = rbf(r1);
+      h[q] = pack_bf2(h0, h1);
+      m[q] = pack_bf2(m0, m1);
+      l[q] = pack_bf2(r0 - m0, r1 - m1);
+    }
+    *(u32x4_t*)hp = h;
+    *(u32x4_t*)mp = m;
+    *(u32x4_t*)lp = l;
+  };
+  load(0);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < KPA / 8; ++v)
+      split8(ra[2 * v], ra[2 * v + 1], Ah + arow * LS + ak + 8 * v, Am + arow * LS + ak + 8 * v,
+             Al + arow * LS + ak + 8 * v);
+#pragma unroll
+    for (int v = 0; v < KPB / 8; ++v)
+      split8(rb[2 * v], rb[2 * v + 1], Bh + brow * LS + bk + 8 * v, Bm + brow * LS + bk + 8 * v,
+             Bl + brow * LS + bk + 8 * v);
+    __syncthreads();
+    if (k0 + BK < kend) load(k0 + BK - kbeg);  // next K tile in flight during the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ko = kk * 16 + 8 * (lane >> 5);
+      bf16x8_t ah[MI], am[MI], al[MI], bh[NJ], bm[NJ], bl[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int r = wm * (TM / 2) + i * 32 + (lane & 31);
+        ah[i] = *(const bf16x8_t*)(Ah + r * LS + ko);
+        am[i] = *(const bf16x8_t*)(Am + r * LS + ko);
+        al[i] = *(const bf16x8_t*)(Al + r * LS + ko);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int r = wn * (TN / 2) + j * 32 + (lane & 31);
+        bh[j] = *(const bf16x8_t*)(Bh + r * LS + ko);
+        bm[j] = *(const bf16x8_t*)(Bm + r * LS + ko);
+        bl[j] = *(const bf16x8_t*)(Bl + r * LS + ko);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          f32x16_t c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
+        }
+    }
+  }
+  // epilogue (as gemm_f32_kernel): lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * (TN / 2) + j * 32 + (lane & 31);
+    if (n >= g.N) continue;
+    const float bias = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (TM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;
+        if (g.ksplit > 1) {
+          g.part[((size_t)blockIdx.y * g.M + m) * g.N + n] = acc[i][j][r];
+          continue;
+        }
+        float v = acc[i][j][r] + bias;
+        if (g.act == 1) v = v / (1.0f + expf(-v));
+        if (g.resid) v = g.resid[(size_t)m * g.ldc + n] + v;
+        g.C[(size_t)m * g.ldc + n] = v;
+      }
+  }
+}
+
+// split-K as launch_split, for the bf16x3 kernel (K chunks multiples of 32)
+template <int TM, int TN>
+static void launch_split_bx3(GemmF32Args g, int target, hipStream_t s) {
+  const int grid = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
+  int S = 1;
+  if (g.part != nullptr && grid < target * 3 / 4 && g.K >= 512) {
+    S = std::min(16, std::max(1, (target + grid - 1) / grid));
+    S = std::min(S, g.K / 256);
+    while (S > 1 && (size_t)S * g.M * g.N > g.part_elems) --S;
+  }
+  if (S <= 1) {
+    g.ksplit = 1; g.kchunk = g.K;
+    hipLaunchKernelGGL((gemm_bx3_kernel<TM, TN>), dim3(grid), dim3(256), 0, s, g);
+    return;
+  }
+  g.kchunk = ((g.K + S - 1) / S + 31) / 32 * 32;
+  S = (g.K + g.kchunk - 1) / g.kchunk;
+  g.ksplit = S;
+  hipLaunchKernelGGL((gemm_bx3_kernel<TM, TN>), dim3(grid, S), dim3(256), 0, s, g);
+  const long long n = (long long)g.M * g.N;
+  hipLaunchKernelGGL(gemm_f32_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g.part, S,
+                     g.M, g.N, g.bias, g.act, g.resid, g.C, g.ldc);
+}
+
 void launch_gemm_f32(const GemmF32Args& g, hipStream_t s) {
   static const int target = getenv("TTS_CODEC_SPLIT_TARGET") ? atoi(getenv("TTS_CODEC_SPLIT_TARGET")) : 768;
+  // TTS_CODEC_BX3=0: plain fp32 MFMA for every contraction
+  static const bool bx3 = !(getenv("TTS_CODEC_BX3") && !atoi(getenv("TTS_CODEC_BX3")));
   const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+  if (bx3 && g.K % 32 == 0 && g.lda % 4 == 0) {
+    if (big >= 256) launch_split_bx3<128, 128>(g, target, s);
+    else launch_split_bx3<64, 64>(g, target, s);
+    return;
+  }
   if (big >= 256) launch_split<128, 128>(g, target, s);
   else launch_split<64, 64>(g, target, s);
 }
