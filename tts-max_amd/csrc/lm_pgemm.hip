@@ -156,10 +156,16 @@ void launch_pgemm(const PgemmArgs& a_in, int epi, int num_cu, hipStream_t s) {
   // 64-row blocks while that still leaves > 2 blocks per CU's worth of weight re-reads
   // unneeded (short prompts), 128-row blocks for long batched prefill
   const bool tall = a.M > 512;
+  auto grid = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * (a.N / bn); };
   if (wide && tall) launch_pgemm_mn<4, 4>(a, epi, s);
-  else if (wide) launch_pgemm_mn<2, 4>(a, epi, s);
+  else if (wide && grid(64, 128) >= num_cu) launch_pgemm_mn<2, 4>(a, epi, s);
   else if (tall) launch_pgemm_mn<4, 2>(a, epi, s);
-  else launch_pgemm_mn<2, 2>(a, epi, s);
+  // short prompts: smaller blocks until the grid covers the CUs (a single prompt's QKV /
+  // o_proj / down gave 64-96 workgroups).  The block shape never changes an output's
+  // k-order (one MFMA accumulation chain over K), so rows stay bit-identical across shapes
+  else if (grid(64, 64) >= num_cu) launch_pgemm_mn<2, 2>(a, epi, s);
+  else if (grid(32, 64) >= num_cu / 2 || epi == EPI_SWIGLU) launch_pgemm_mn<1, 2>(a, epi, s);  // (SwiGLU: n-tile pairs)
+  else launch_pgemm_mn<1, 1>(a, epi, s);
 }
 
 }  // namespace tts
