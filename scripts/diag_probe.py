@@ -11,8 +11,8 @@ import json, os, sys
 sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
 from tts_amd import configs
 from tts_amd.speechlm import MI355XSpeechLM
-m = MI355XSpeechLM.synthetic(configs.TTS1, max_batch=1, max_seq_len=720)
 rows = int(sys.argv[2])
+m = MI355XSpeechLM.synthetic(configs.TTS1, max_batch=rows, max_seq_len=720)
 print(json.dumps({k: round(m.bench_kernel(k, rows=rows, ctx=450, iters=64)[0] * 1000, 2) for k in m.KERNELS}))
 '''
 rows = os.environ.get("ROWS", "1")
