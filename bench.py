@@ -171,8 +171,17 @@ def main():
     for k in lm.KERNELS:
         ms, by = lm.bench_kernel(k, rows=B, ctx=ctx_mid, iters=args.kernel_iters)
         kern[k] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
-    # per-step share: qkv/o/gate_up/down/attention once per layer, lm_head once
-    share = {k: v["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k, v in kern.items()}
+    # the one-row step runs QKV with the attention fused in (one launch for both)
+    fused = False
+    try:
+        ms, by = lm.bench_kernel("qkv_attn", rows=B, ctx=ctx_mid, iters=args.kernel_iters)
+        kern["qkv_attn"] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
+        fused = True
+    except Exception:  # noqa: BLE001 (not this shape: separate launches)
+        pass
+    # per-step share: the layer kernels once per layer, lm_head once
+    in_step = [k for k in kern if not (fused and k in ("qkv", "attention"))]
+    share = {k: kern[k]["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k in in_step}
     dom = max(share, key=share.get)
     step_ms = lm_decode / max(dec_steps, 1)
     kv_ctx_bytes = B * arch.kv_bytes_per_token() * ctx_mid
