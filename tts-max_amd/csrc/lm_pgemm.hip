@@ -25,7 +25,7 @@ TTS_DEV bf16x8_t as_bf16x8p(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v);
 constexpr int PK_KK = 2;                // k-tiles per K step
 constexpr int PK_LDA = PK_KK * 32 + 8;  // LDS row stride of A (bf16): +16 B spreads the rows' banks
 
-template <int MW, int NW, int EPI>
+template <int MW, int NW, int EPI, bool DEEP = (MW <= 2)>
 __global__ __launch_bounds__(256) void pgemm_kernel(PgemmArgs a) {
   constexpr int BM = 2 * MW * 16, BN = 2 * NW * 16;
   constexpr int NTB = BN / 16;                     // n-tiles per workgroup
@@ -42,13 +42,17 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgemmArgs a) {
   const int m0 = mb * BM, nt0 = nbk * NTB;
   const int KT = a.K >> 5, steps = KT / PK_KK;
 
-  u32x4_t ra[ACH], rb[BCH];
-  auto load = [&](int s) {
+  // Two register sets of staged operands: the global loads of step s+2 are issued while
+  // step s computes (one step of MFMAs is shorter than an HBM round trip), and unconditional
+  // (clamped step index) so the vmcnt waits stay exact.  Requires an even step count.
+  u32x4_t ra[DEEP ? 2 : 1][ACH], rb[DEEP ? 2 : 1][BCH];
+  auto load = [&](int s, u32x4_t (&xa)[ACH], u32x4_t (&xb)[BCH]) {
+    s = min(s, steps - 1);
 #pragma unroll
     for (int j = 0; j < ACH; ++j) {
       const int c = tid + j * 256, row = c / (PK_KK * 4), col = (c % (PK_KK * 4)) * 8;
       const int m = min(m0 + row, a.M - 1);
-      ra[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + s * PK_KK * 32 + col);
+      xa[j] = *(const u32x4_t*)(a.x + (size_t)m * a.ldx + s * PK_KK * 32 + col);
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
@@ -56,17 +60,17 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgemmArgs a) {
       const int ntl = t / PK_KK, ktl = t % PK_KK;
       const long long tile =
           plan_tile(a.ng, a.ksplit, a.ku, a.ur, a.units, KT, a.kc, nt0 + ntl, s * PK_KK + ktl);
-      rb[j] = __builtin_nontemporal_load((const u32x4_t*)a.w + tile * 64 + ln);
+      xb[j] = __builtin_nontemporal_load((const u32x4_t*)a.w + tile * 64 + ln);
     }
   };
-  auto stash = [&](int buf) {
+  auto stash = [&](int buf, const u32x4_t (&xa)[ACH], const u32x4_t (&xb)[BCH]) {
 #pragma unroll
     for (int j = 0; j < ACH; ++j) {
       const int c = tid + j * 256, row = c / (PK_KK * 4), col = (c % (PK_KK * 4)) * 8;
-      *(u32x4_t*)(&As[buf][row * PK_LDA + col]) = ra[j];
+      *(u32x4_t*)(&As[buf][row * PK_LDA + col]) = xa[j];
     }
 #pragma unroll
-    for (int j = 0; j < BCH; ++j) Bs[buf][tid + j * 256] = rb[j];
+    for (int j = 0; j < BCH; ++j) Bs[buf][tid + j * 256] = xb[j];
   };
 
   f32x4_t acc[MW][NW];
@@ -75,12 +79,7 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgemmArgs a) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
-  stash(0);
-  __syncthreads();
-  for (int s = 0; s < steps; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < steps) load(s + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int ktl = 0; ktl < PK_KK; ++ktl) {
       bf16x8_t bf[NW];
@@ -95,8 +94,35 @@ __global__ __launch_bounds__(256) void pgemm_kernel(PgemmArgs a) {
         for (int j = 0; j < NW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (s + 1 < steps) stash(buf ^ 1);
+  };
+
+  if constexpr (!DEEP) {  // tall blocks: one step ahead (the second set would cost occupancy)
+    load(0, ra[0], rb[0]);
+    stash(0, ra[0], rb[0]);
     __syncthreads();
+    for (int s = 0; s < steps; ++s) {
+      const int buf = s & 1;
+      if (s + 1 < steps) load(s + 1, ra[0], rb[0]);
+      compute(buf);
+      if (s + 1 < steps) stash(buf ^ 1, ra[0], rb[0]);
+      __syncthreads();
+    }
+  } else {
+  load(0, ra[0], rb[0]);
+  load(1, ra[1], rb[1]);
+  stash(0, ra[0], rb[0]);
+  __syncthreads();
+  load(2, ra[0], rb[0]);
+  for (int s = 0; s < steps; s += 2) {
+    compute(0);                    // step s (buffer 0); set 1 holds step s+1, set 0 step s+2
+    stash(1, ra[1], rb[1]);
+    __syncthreads();
+    load(s + 3, ra[1], rb[1]);
+    compute(1);                    // step s+1
+    stash(0, ra[0], rb[0]);        // (after the last step: a clamped duplicate, never used)
+    __syncthreads();
+    load(s + 4, ra[0], rb[0]);
+  }
   }
 
   // ---- epilogue: lane owns column (lane & 15) of each n-tile, rows 4*(lane>>4) + r
@@ -143,7 +169,7 @@ void launch_pgemm_mn(const PgemmArgs& a, int epi, hipStream_t s) {
 }  // namespace
 
 bool pgemm_supported(int M, int N, int K, int epi) {
-  return M >= 1 && (N % 64) == 0 && (K % (PK_KK * 32)) == 0 &&
+  return M >= 1 && (N % 64) == 0 && (K % (2 * PK_KK * 32)) == 0 &&  // (an even step count)
          (epi == EPI_STORE || epi == EPI_RESID || epi == EPI_SWIGLU);
 }
 
