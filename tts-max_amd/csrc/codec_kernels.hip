@@ -225,17 +225,21 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 ra[KPA / 4], rb[KPB / 4];
-  auto load = [&](int kn) {
+  // two register sets: the global loads of step s+2 are in flight while step s computes
+  // (unconditional, step index clamped: exact vmcnt waits)
+  const int nsteps = (kend - kbeg) / BK;
+  float4 ra[2][KPA / 4], rb[2][KPB / 4];
+  auto load = [&](int st, float4 (&xa)[KPA / 4], float4 (&xb)[KPB / 4]) {
+    const int kn = min(st, nsteps - 1) * BK;
 #pragma unroll
     for (int v = 0; v < KPA / 4; ++v) {
       const float4 l = *(const float4*)(ap + kn + 4 * v);
-      ra[v] = aok ? l : z4;
+      xa[v] = aok ? l : z4;
     }
 #pragma unroll
     for (int v = 0; v < KPB / 4; ++v) {
       const float4 l = *(const float4*)(bp + kn + 4 * v);
-      rb[v] = bok ? l : z4;
+      xb[v] = bok ? l : z4;
     }
   };
   // 8 fp32 -> 8 bf16 each of h, m, l (exact residuals: x - h and x - h - m are fp32-exact),
@@ -256,19 +260,17 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
     *(u32x4_t*)mp = m;
     *(u32x4_t*)lp = l;
   };
-  load(0);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
+  auto stage = [&](const float4 (&xa)[KPA / 4], const float4 (&xb)[KPB / 4]) {
 #pragma unroll
     for (int v = 0; v < KPA / 8; ++v)
-      split8(ra[2 * v], ra[2 * v + 1], Ah + arow * LS + ak + 8 * v, Am + arow * LS + ak + 8 * v,
+      split8(xa[2 * v], xa[2 * v + 1], Ah + arow * LS + ak + 8 * v, Am + arow * LS + ak + 8 * v,
              Al + arow * LS + ak + 8 * v);
 #pragma unroll
     for (int v = 0; v < KPB / 8; ++v)
-      split8(rb[2 * v], rb[2 * v + 1], Bh + brow * LS + bk + 8 * v, Bm + brow * LS + bk + 8 * v,
+      split8(xb[2 * v], xb[2 * v + 1], Bh + brow * LS + bk + 8 * v, Bm + brow * LS + bk + 8 * v,
              Bl + brow * LS + bk + 8 * v);
-    __syncthreads();
-    if (k0 + BK < kend) load(k0 + BK - kbeg);  // next K tile in flight during the MFMAs
+  };
+  auto compute = [&]() {
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       const int ko = kk * 16 + 8 * (lane >> 5);
@@ -300,6 +302,20 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
         }
     }
+  };
+  load(0, ra[0], rb[0]);
+  load(1, ra[1], rb[1]);
+  for (int st = 0; st < nsteps; st += 2) {
+    __syncthreads();
+    stage(ra[0], rb[0]);
+    __syncthreads();
+    load(st + 2, ra[0], rb[0]);
+    compute();
+    __syncthreads();
+    stage(ra[1], rb[1]);  // (an odd last step stages a clamped duplicate, not computed)
+    __syncthreads();
+    load(st + 3, ra[1], rb[1]);
+    if (st + 1 < nsteps) compute();
   }
   // epilogue (as gemm_f32_kernel): lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
