@@ -412,7 +412,52 @@ void launch_attn_decode(const AttnArgs& a, bool fused, hipStream_t s) {
   }
 }
 
+// The same merge with every chunk statistic and partial of a (row, head) issued at once
+// (NSX chunks, clamped; a runtime-length loop would serialise one L2 round trip per chunk
+// and pass): one wave per head, four heads per workgroup.  Same formula and order as
+// attn_combine_kernel, so the bits are identical.
+template <int D, int NSX>
+__global__ __launch_bounds__(256) void attn_combine_wide_kernel(AttnArgs a) {
+  constexpr int DPL = D / 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rh = blockIdx.x * 4 + wave;  // (row, head)
+  if (rh >= a.rows * a.H) return;
+  const int row = rh / a.H, h = rh % a.H;
+  const int ctx = a.row_pos[row] + 1;
+  const int ns = (ctx + a.split - 1) / a.split;
+  const size_t pbase = ((size_t)row * a.H + h) * a.nsplit;
+  float2 ml[NSX];
+  float ov[NSX][DPL];
+#pragma unroll
+  for (int i = 0; i < NSX; ++i) {
+    const size_t pi = pbase + min(i, ns - 1);
+    ml[i] = *(const float2*)(a.part_ml + pi * 2);
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) ov[i][e] = a.part_o[pi * D + lane + 64 * e];
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NSX; ++i) if (i < ns) m = fmaxf(m, ml[i].x);
+  float l = 0.f;
+#pragma unroll
+  for (int i = 0; i < NSX; ++i) if (i < ns) l += ml[i].y * expf(ml[i].x - m);
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) {
+    float o = 0.f;
+#pragma unroll
+    for (int i = 0; i < NSX; ++i) if (i < ns) o += ov[i][e] * expf(ml[i].x - m);
+    a.out[(size_t)row * a.H * D + h * D + lane + 64 * e] = f2bf(o / l);
+  }
+}
+
 void launch_attn_combine(const AttnArgs& a, hipStream_t s) {
+  // (every row's chunk count <= 8 whenever the allocated chunk count is)
+  if (a.nsplit <= 8) {
+    const dim3 g((a.rows * a.H + 3) / 4);
+    if (a.D == 64) hipLaunchKernelGGL((attn_combine_wide_kernel<64, 8>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_combine_wide_kernel<128, 8>), g, dim3(256), 0, s, a);
+    return;
+  }
   if (a.D == 64) hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(a.rows * a.H), dim3(64), 0, s, a);
   else hipLaunchKernelGGL(attn_combine_kernel<128>, dim3(a.rows * a.H), dim3(128), 0, s, a);
 }
