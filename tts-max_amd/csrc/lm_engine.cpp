@@ -362,7 +362,7 @@ struct Ctx {
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
       if (p.sliced) a.part_out = w.kpart.as<float>();
-      const bool fuse_norm = p.sliced && epi == EPI_RESID && next_norm && m > 16 && rows <= 32;
+      const bool fuse_norm = p.sliced && epi == EPI_RESID && next_norm && m > 16 && rows <= 32 && N <= 8192;
       if (fuse_norm) {
         a.next_norm = next_norm;
         a.norm_out = w.xn.as<bf16_t>() + (size_t)r0 * ldo;

@@ -162,7 +162,7 @@ void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s);
 // K-sliced GEMM combine: v = bf16(sum_c part[c][m][n]);  resid ? resid += v : out = v
 void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
                            bf16_t* resid, int ldo, hipStream_t s);
-// residual combine + the next RMSNorm of the updated rows into xn (N % 8 == 0, N <= 32768)
+// residual combine + the next RMSNorm of the updated rows into xn (N % 8 == 0, N <= 8192)
 void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp, bf16_t* resid, int ldo,
                                 const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s);
 

@@ -33,9 +33,61 @@ __global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, int ldx, const bf16
   }
 }
 
+// The same normalisation with the row and the weight loaded once, both issued at entry
+// (K <= 256 * 8 * RJ): one memory round trip instead of two.  Chunk c = tid + 256 j lands in
+// 512-value segment c / 64 on wave (c / 64) % 4 exactly as above: identical sums and bits.
+template <int RJ>
+__global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const bf16_t* __restrict__ x, int ldx,
+                                                          const bf16_t* __restrict__ w, float eps,
+                                                          bf16_t* __restrict__ y, int ldy, int K) {
+  __shared__ float segs[64];
+  const bf16_t* xr = x + (size_t)blockIdx.x * ldx;
+  bf16_t* yr = y + (size_t)blockIdx.x * ldy;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int nch = K / 8;
+  u32x4_t v[RJ], g[RJ];
+#pragma unroll
+  for (int j = 0; j < RJ; ++j) {  // unconditional (clamped) loads
+    const int c = min(tid + 256 * j, nch - 1);
+    v[j] = *(const u32x4_t*)(xr + c * 8);
+    g[j] = *(const u32x4_t*)(w + c * 8);
+  }
+#pragma unroll
+  for (int j = 0; j < RJ; ++j) {
+    const int c0 = 256 * j + (tid & ~63);  // first chunk of this wave's segment
+    if (c0 < nch) {                          // (wave-uniform)
+      const float s = wave_sum_dpp(tid + 256 * j < nch ? chunk_sumsq(v[j]) : 0.f);
+      if (lane == 0) segs[c0 >> 6] = s;
+    }
+  }
+  __syncthreads();
+  const int nseg = (K + 511) / 512;
+  float ss = 0.f;
+  for (int sg = 0; sg < nseg; ++sg) ss += segs[sg];
+  const float r = 1.0f / sqrtf(ss / (float)K + eps);
+#pragma unroll
+  for (int j = 0; j < RJ; ++j) {
+    const int c = tid + 256 * j;
+    if (c < nch) {
+      u32x4_t o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        o[q] = pack_bf2(rbf(bf_lo(g[j][q]) * rbf(bf_lo(v[j][q]) * r)), rbf(bf_hi(g[j][q]) * rbf(bf_hi(v[j][q]) * r)));
+      *(u32x4_t*)(yr + c * 8) = o;
+    }
+  }
+}
+
 void launch_rmsnorm(const bf16_t* x, int ldx, const bf16_t* w, float eps, bf16_t* y, int ldy,
                     int M, int K, hipStream_t s) {
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
+  if (K % 8 == 0 && K <= 2048)
+    hipLaunchKernelGGL((rmsnorm_reg_kernel<1>), dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
+  else if (K % 8 == 0 && K <= 4096)
+    hipLaunchKernelGGL((rmsnorm_reg_kernel<2>), dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
+  else if (K % 8 == 0 && K <= 8192)
+    hipLaunchKernelGGL((rmsnorm_reg_kernel<4>), dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
 }
 
 __global__ void embed_kernel(const int* __restrict__ tokens, const bf16_t* __restrict__ table,
@@ -206,29 +258,35 @@ __global__ __launch_bounds__(256) void splitk_combine_norm_kernel(
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nchunk = N / 8;  // 8-column chunks; wave w takes 512-value segments w, w + 4, ...
   bf16_t* r = resid + (size_t)m * ldo;
-  for (int base = wave * 64; base < nchunk; base += 256) {  // wave-uniform: full DPP rows
+  constexpr int IT = 4;      // N <= 8192: the updated chunks stay in registers for the norm
+  u32x4_t keep[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int base = wave * 64 + it * 256;
+    if (base >= nchunk) break;  // wave-uniform: full DPP rows
     const int c = base + lane;
     float s = 0.f;
     if (c < nchunk) {
-    const int n = c * 8;
-    float v[8];
-    {
-      const float4* p = (const float4*)(part + (size_t)m * ldp + n);
-      const float4 a = p[0], b = p[1];
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    }
-    for (int k = 1; k < kc; ++k) {
-      const float4* p = (const float4*)(part + ((size_t)k * M + m) * ldp + n);
-      const float4 a = p[0], b = p[1];
-      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-    }
-    const u32x4_t old = *(const u32x4_t*)(r + n);
-    u32x4_t pk;
+      const int n = c * 8;
+      float v[8];
+      {
+        const float4* p = (const float4*)(part + (size_t)m * ldp + n);
+        const float4 a = p[0], b = p[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      for (int k = 1; k < kc; ++k) {
+        const float4* p = (const float4*)(part + ((size_t)k * M + m) * ldp + n);
+        const float4 a = p[0], b = p[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      const u32x4_t old = *(const u32x4_t*)(r + n);
+      u32x4_t pk;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      pk[q] = pack_bf2(bf_lo(old[q]) + rbf(v[2 * q]), bf_hi(old[q]) + rbf(v[2 * q + 1]));
-    *(u32x4_t*)(r + n) = pk;
-    s = chunk_sumsq(pk);
+      for (int q = 0; q < 4; ++q)
+        pk[q] = pack_bf2(bf_lo(old[q]) + rbf(v[2 * q]), bf_hi(old[q]) + rbf(v[2 * q + 1]));
+      *(u32x4_t*)(r + n) = pk;
+      keep[it] = pk;
+      s = chunk_sumsq(pk);
     }
     s = wave_sum_dpp(s);
     if (lane == 0) segs[base >> 6] = s;
@@ -237,11 +295,12 @@ __global__ __launch_bounds__(256) void splitk_combine_norm_kernel(
   float ss = 0.f;
   for (int sg = 0; sg < (nchunk + 63) / 64; ++sg) ss += segs[sg];
   const float rs = 1.0f / sqrtf(ss / (float)N + eps);
-  for (int base = wave * 64; base < nchunk; base += 256) {  // the chunks this thread wrote
-    const int c = base + lane;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {  // the chunks this thread wrote
+    const int c = wave * 64 + it * 256 + lane;
     if (c >= nchunk) break;
     const int n = c * 8;
-    u32x4_t v = *(const u32x4_t*)(r + n);
+    u32x4_t v = keep[it];
     const u32x4_t g = *(const u32x4_t*)(normw + n);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
