@@ -127,7 +127,10 @@ __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* 
   __shared__ int si[4];
   __shared__ int stok;
   const int b = blockIdx.x;
-  if (st.done[b]) return;
+  // the row's state is read with the partials (one round trip), not after the reduction
+  const int done = st.done[b];
+  int g0 = 0, lim = 0, pos0 = 0;
+  if (threadIdx.x == 0) { g0 = st.gen_count[b]; lim = st.limit[b]; pos0 = st.pos[b]; }
   float v = -INFINITY;
   int i = 0x7fffffff;
   for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
@@ -135,6 +138,7 @@ __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* 
     const int i2 = pi[(size_t)b * part_stride + p];
     if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
   }
+  if (done) return;  // (uniform)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float v2 = __shfl_xor(v, o, 64);
@@ -148,14 +152,14 @@ __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* 
       if (sv[w] > v || (sv[w] == v && si[w] < i)) { v = sv[w]; i = si[w]; }
     // all-(-inf) rows cannot happen (only EOS is masked); guard anyway
     const int tok = (i == 0x7fffffff) ? 0 : i;
-    const int g = st.gen_count[b];
+    const int g = g0;
     st.out_ids[(size_t)b * st.out_stride + g] = tok;
     st.gen_count[b] = g + 1;
     st.seen[(size_t)b * st.seen_stride + (tok >> 5)] |= 1u << (tok & 31);
     if (st.counts) st.counts[(size_t)b * st.seen_stride * 32 + tok] += 1;
     st.tokens[b] = tok;
-    st.pos[b] += 1;
-    const bool stop = (tok == st.eos_id) || (g + 1 >= st.limit[b]);
+    st.pos[b] = pos0 + 1;
+    const bool stop = (tok == st.eos_id) || (g + 1 >= lim);
     st.eos_mask[b] = (g + 1 < st.min_new) ? st.eos_id : -1;
     if (stop) {
       st.done[b] = 1;
