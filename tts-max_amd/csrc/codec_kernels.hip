@@ -11,6 +11,7 @@
 // window: row t starts at x + (t - k/2)*C and spans k*C contiguous floats (lda = C < K).
 // No im2col buffer is ever written.
 #include <algorithm>
+#include <stdexcept>
 
 #include "codec_kernels.h"
 #include "hip_common.h"
@@ -409,16 +410,18 @@ __global__ void groupnorm_stats_kernel(const float* __restrict__ x, int T, int C
   __shared__ float red[16];
   const int grp = blockIdx.x;
   const long long n = (long long)T * cg;
+  // thread -> (column c of the group, rows t0, t0 + rs, ...): no per-element integer
+  // division, independent loads (the launcher guarantees blockDim % cg == 0)
+  const int c = threadIdx.x % cg, t0 = threadIdx.x / cg, rs = blockDim.x / cg;
+  const float* xc = x + grp * cg + c;
   float sum = 0.f;
-  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
-    const int t = (int)(i / cg), c = (int)(i % cg);
-    sum += x[(size_t)t * C + grp * cg + c];
-  }
+#pragma unroll 4
+  for (int t = t0; t < T; t += rs) sum += xc[(size_t)t * C];
   const float mean = block_sum(sum, red) / (float)n;
   float sq = 0.f;
-  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
-    const int t = (int)(i / cg), c = (int)(i % cg);
-    const float d = x[(size_t)t * C + grp * cg + c] - mean;
+#pragma unroll 4
+  for (int t = t0; t < T; t += rs) {
+    const float d = xc[(size_t)t * C] - mean;
     sq += d * d;
   }
   const float var = block_sum(sq, red) / (float)n;
@@ -430,8 +433,9 @@ __global__ void groupnorm_stats_kernel(const float* __restrict__ x, int T, int C
 
 void launch_groupnorm_stats(const float* x, int T, int C, int groups, float eps, float* stats,
                             hipStream_t s) {
-  hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(groups), dim3(1024), 0, s, x, T, C,
-                     C / groups, eps, stats);
+  const int cg = C / groups;
+  if (cg > 1024 || 1024 % cg != 0) throw std::runtime_error("groupnorm: channels per group must divide 1024");
+  hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(groups), dim3(1024), 0, s, x, T, C, cg, eps, stats);
 }
 
 __global__ void groupnorm_swish_kernel(const float* __restrict__ x, int T, int C, int cg,
