@@ -95,7 +95,10 @@ typedef struct {
   int32_t max_seq_len;         /* KV capacity per sequence (prompt + generated)      */
 } tts_lm_config;
 
-/* Loads the SpeechLM.  Weights are bf16 (or f32 / f16, converted to bf16 on load).
+/* Loads the SpeechLM.  Weights are bf16, or f32 / f16 converted to bf16 on load (one RNE
+ * rounding; lossless for f16 weights that came from the bf16 training checkpoint).  The
+ * engine always computes in bf16 with fp32 accumulation — the reference serving CLI's
+ * fp16 arithmetic (tools/serving/inference.py:103-107) is not reproduced.
  * Optional tensors "rope.cos" / "rope.sin" ([max_seq_len, head_dim], bf16) override the
  * engine-computed RoPE table (the Python host passes the table computed exactly as
  * LlamaRotaryEmbedding.forward does).  Optional "vocab.id_to_code" (int32 [vocab]) is the
@@ -156,6 +159,11 @@ tts_status tts_generate_read(tts_engine* e, int32_t* out_ids, int32_t out_stride
 tts_status tts_slots_open(tts_engine* e, const tts_gen_params* p, int32_t n_slots, void* stream);
 tts_status tts_slots_add(tts_engine* e, int32_t slot, const int32_t* prompt_ids, int32_t prompt_len,
                          int32_t max_new_tokens);
+/* As tts_slots_add with the request's own sampling key (vLLM SamplingParams.seed): the
+ * same key and prompt draw the same tokens whatever else the batch holds.  tts_slots_add
+ * derives a distinct key per admitted request from the batch seed (p->seed). */
+tts_status tts_slots_add_seeded(tts_engine* e, int32_t slot, const int32_t* prompt_ids, int32_t prompt_len,
+                                int32_t max_new_tokens, uint64_t seed);
 tts_status tts_slots_step(tts_engine* e, int32_t n_steps, int32_t* n_active);
 tts_status tts_slots_read(tts_engine* e, int32_t slot, int32_t* out_ids, int32_t capacity, int32_t* n_out,
                           int32_t* finished);

@@ -22,6 +22,7 @@ and records the agreement in tests/golden/manifest.json.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -53,17 +54,16 @@ CODEC_CASES = {
     "codec_16k": ("xcodec2-16k", 0xC0DEC + 1, [40]),
     "codec_48k": ("codec-48k", 0xC0DEC + 2, [30]),
     "codec_24k_d2": ("codec-24k-d2", 0xC0DEC + 3, [50, 3]),
+    # the bench's codec leg (650 codes = 150 prompt + 500 generated; 11 key chunks of 64 in
+    # the codec attention) and three lengths between
+    "codec_24k_long": ("codec-24k", 0xC0DEC, [650, 300, 130, 65]),
 }
 
 
-def lm_fixture(name: str, manifest: dict) -> None:
+def hf_model(arch, w):
+    """transformers LlamaForCausalLM (bf16, CPU) holding the synthetic weights `w`."""
     from transformers import LlamaConfig, LlamaForCausalLM
 
-    arch_name, seed, prompts, settings = LM_CASES[name]
-    arch = configs.LM_ARCHS[arch_name]
-    vocab = configs.vocab_for(arch)
-    t0 = time.time()
-    w = synth.lm_weights_cpu(arch, seed)
     cfg = LlamaConfig(**arch.hf_config_dict())
     with torch.device("meta"):
         model = LlamaForCausalLM(cfg)
@@ -76,6 +76,32 @@ def lm_fixture(name: str, manifest: dict) -> None:
     assert not missing and not unexpected, (missing, unexpected)
     model.model.rotary_emb = type(model.model.rotary_emb)(cfg)  # buffers were on meta
     model.eval()
+    return model
+
+
+def hf_generate(model, prompt, max_length, min_new, eos, rep):
+    """The reference call (inferencing.py:94-107, greedy) -> (new ids, per-step top-2 margins
+    of the processed scores, per-step (top1, top2) ids)."""
+    with torch.no_grad():
+        out = model.generate(input_ids=torch.tensor([prompt]), max_length=max_length, min_new_tokens=min_new,
+                             eos_token_id=eos, do_sample=False, repetition_penalty=rep, top_p=1.0,
+                             temperature=0.0, output_scores=True, return_dict_in_generate=True)
+    new = out.sequences[0, len(prompt):].tolist()
+    margins, tops = [], []
+    for sc in out.scores:  # processed scores (penalty + min-new mask) of each step
+        top = torch.topk(sc[0].float(), 2)
+        margins.append(float(top.values[0] - top.values[1]))
+        tops.append([int(i) for i in top.indices])
+    return new, margins, tops
+
+
+def lm_fixture(name: str, manifest: dict) -> None:
+    arch_name, seed, prompts, settings = LM_CASES[name]
+    arch = configs.LM_ARCHS[arch_name]
+    vocab = configs.vocab_for(arch)
+    t0 = time.time()
+    w = synth.lm_weights_cpu(arch, seed)
+    model = hf_model(arch, w)
     orc = lm_oracle.LlamaOracle(arch, w, max_seq_len=4096)
     eos = vocab.speech_end_id
     rec = dict(prompt_ids=[], prompt_lens=[], hf_new=[], hf_new_lens=[], oracle_new=[], oracle_lens=[],
@@ -85,16 +111,7 @@ def lm_fixture(name: str, manifest: dict) -> None:
         prompt = synth.synthetic_prompt(vocab, utt, n_text, n_codes)
         P = len(prompt)
         max_length = P + st["new"]
-        with torch.no_grad():
-            out = model.generate(input_ids=torch.tensor([prompt]), max_length=max_length,
-                                 min_new_tokens=st["min_new"], eos_token_id=eos, do_sample=False,
-                                 repetition_penalty=st["rep"], top_p=1.0, temperature=0.0,
-                                 output_scores=True, return_dict_in_generate=True)
-        hf_new = out.sequences[0, P:].tolist()
-        hf_margins = []
-        for sc in out.scores:  # processed scores (penalty + min-new mask) of each step
-            top = torch.topk(sc[0].float(), 2).values
-            hf_margins.append(float(top[0] - top[1]))
+        hf_new, hf_margins, _ = hf_generate(model, prompt, max_length, st["min_new"], eos, st["rep"])
         rec.setdefault("hf_margins", []).extend(hf_margins)
         o_new, margins = orc.generate(prompt, max_length, st["min_new"], eos, st["rep"])
         agree = 0
@@ -106,11 +123,24 @@ def lm_fixture(name: str, manifest: dict) -> None:
             hf_logits = model(torch.tensor([seq])).logits[0, -8:].float()
         o_logits = orc.score(seq, 8)
         diff = (hf_logits - o_logits).abs().max().item()
+        if arch.vocab_size > 100000:  # engine-vs-transformers logits: top-32 + 32 fixed indices per step
+            n_tf = len(hf_new)
+            with torch.no_grad():
+                tf = model(torch.tensor([seq[:-1]])).logits[0, -n_tf:].float()
+            gen = torch.Generator().manual_seed(utt)
+            idx = torch.cat([torch.topk(tf, 32, dim=-1).indices,
+                             torch.randint(0, arch.vocab_size, (n_tf, 32), generator=gen)], dim=1)
+            rec.setdefault("tf_idx", []).append(idx.numpy().astype(np.int32))
+            rec.setdefault("tf_val", []).append(torch.gather(tf, 1, idx).numpy().astype(np.float32))
+            o_tf = orc.score(seq[:-1], n_tf)
+            tf_oracle_dev = (torch.gather(o_tf, 1, idx) - torch.gather(tf, 1, idx)).abs()
         stats.append(dict(P=P, n_new=len(hf_new), agree_prefix=agree, identical=hf_new == o_new,
                           min_margin=min(margins), hf_min_margin=min(hf_margins),
                           first_hf_near_tie=next((i for i, m in enumerate(hf_margins) if m < 0.25), None),
                           max_abs_logit_diff=diff,
                           logit_scale=hf_logits.abs().max().item()))
+        if arch.vocab_size > 100000:
+            stats[-1].update(tf_oracle_max=float(tf_oracle_dev.max()), tf_oracle_mean=float(tf_oracle_dev.mean()))
         rec["prompt_ids"] += prompt
         rec["prompt_lens"].append(P)
         rec["hf_new"] += hf_new
@@ -122,10 +152,155 @@ def lm_fixture(name: str, manifest: dict) -> None:
         rec["min_new"].append(st["min_new"])
         rec["rep"].append(st["rep"])
         rec["eos"].append(eos)
+    for k in ("tf_idx", "tf_val"):
+        if k in rec:
+            rec[k] = np.concatenate(rec[k])
     np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), arch=arch_name, seed=seed,
                         **{k: np.asarray(v) for k, v in rec.items()})
     manifest[name] = dict(kind="lm", arch=arch_name, seed=seed, generator="transformers.LlamaForCausalLM.generate "
                           f"(transformers {__import__('transformers').__version__}, bf16, CPU, sdpa)",
+                          cases=stats, seconds=round(time.time() - t0, 1))
+    print(name, json.dumps(stats))
+
+
+# decisive greedy parity at the real vocabulary (synth.ChainSpec): TTS-1 dims, 16 layers,
+# V = 193,856.  (utt, chain start, settings, group): "single" cases exercise the penalty /
+# min-new / EOS / no-penalty paths at batch 1; the "batch" group shares settings so the
+# GPU test can run its prompts (and copies of them) as 8..48 rows of one batch.
+CHAIN_CASES = {
+    "lm_chain": ("tts1", 0x5EED, [
+        (0, 300, dict(new=500, min_new=500, rep=1.1), "single"),  # bench shape: 500 codes, EOS masked
+        (1, 200, dict(new=300, min_new=100, rep=1.1), "single"),  # EOS unit 340 -> stops with EOS
+        (2, 60, dict(new=120, min_new=120, rep=1.0), "single"),   # no penalty: lagged ids win
+        (3, 700, dict(new=200, min_new=200, rep=1.4), "single"),  # CLI penalty
+    ] + [(10 + r, 10 + 190 * r, dict(new=500, min_new=500, rep=1.1), "batch") for r in range(8)]),
+}
+
+
+def chain_fixture(name: str, manifest: dict) -> None:
+    arch_name, seed, cases = CHAIN_CASES[name]
+    arch = configs.LM_ARCHS[arch_name]
+    vocab = configs.vocab_for(arch)
+    spec = synth.ChainSpec()
+    t0 = time.time()
+    w = synth.lm_weights_cpu(arch, seed)
+    synth.apply_chain(w, arch, spec)
+    model = hf_model(arch, w)
+    orc = lm_oracle.LlamaOracle(arch, w, max_seq_len=4096)
+    eos = vocab.speech_end_id
+    rec = dict(prompt_ids=[], prompt_lens=[], hf_new=[], hf_new_lens=[], hf_margins=[], hf_top2=[], max_length=[],
+               min_new=[], rep=[], eos=[], group=[], start=[])
+    stats = []
+    for utt, start, st, group in cases:
+        prompt = synth.chain_prompt(vocab, spec, utt, start, 30 + utt % 7, 120 + 3 * utt)
+        P = len(prompt)
+        new, margins, tops = hf_generate(model, prompt, P + st["new"], st["min_new"], eos, st["rep"])
+        # the decision noise: HF vs the oracle, teacher-forced, on each step's top-2 logits
+        seq = prompt + new
+        n_tf = min(len(new), 24)
+        with torch.no_grad():
+            tf = model(torch.tensor([seq[:-1]])).logits[0, -n_tf:].float()
+        o_tf = orc.score(seq[:-1], n_tf)
+        top2 = torch.tensor(tops[-n_tf:])
+        dev = (torch.gather(tf, 1, top2) - torch.gather(o_tf, 1, top2)).abs()
+        stats.append(dict(utt=utt, start=start, group=group, P=P, n_new=len(new), ends_with_eos=new[-1] == eos,
+                          hf_min_margin=min(margins), top2_dev_vs_oracle_max=float(dev.max()), **st))
+        rec["prompt_ids"] += prompt
+        rec["prompt_lens"].append(P)
+        rec["hf_new"] += new
+        rec["hf_new_lens"].append(len(new))
+        rec["hf_margins"] += margins
+        rec["hf_top2"] += tops
+        rec["max_length"].append(P + st["new"])
+        rec["min_new"].append(st["min_new"])
+        rec["rep"].append(st["rep"])
+        rec["eos"].append(eos)
+        rec["group"].append(group)
+        rec["start"].append(start)
+        print(name, json.dumps(stats[-1]), flush=True)
+    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), arch=arch_name, seed=seed,
+                        chain=json.dumps(dataclasses.asdict(spec)), **{k: np.asarray(v) for k, v in rec.items()})
+    manifest[name] = dict(kind="lm_chain", arch=arch_name, seed=seed, chain=dataclasses.asdict(spec),
+                          generator="transformers.LlamaForCausalLM.generate "
+                          f"(transformers {__import__('transformers').__version__}, bf16, CPU, sdpa) on the chain "
+                          "model (synth.apply_chain)", cases=stats, seconds=round(time.time() - t0, 1))
+
+
+# The synthesis composition (inferencing.py:110-159) executed by the reference's own
+# `_synthesize_audio`: transformers' generate on the tiny LM, the reference codec loaded by
+# its own `decoding.create` from a {"model": ...} checkpoint, a duck-typed tokenizer that
+# hands over the prompt ids and names ids like the real one (<|s_N|>, other added tokens).
+# (utt, n_text, n_prompt_codes, max_new, min_new, rep)
+SYNTH_CASES = {"synth_tiny": ("tiny", 11, "codec-24k", 0xC0DEC,
+                                 [(0, 12, 20, 40, 10, 1.1), (1, 5, 4, 24, 0, 1.4), (2, 30, 50, 48, 48, 1.0)])}
+
+
+class _IdTokenizer:
+    """The three tokenizer calls _synthesize_audio makes (inferencing.py:122,126,149)."""
+
+    def __init__(self, vocab, prompt_ids):
+        self.vocab, self.prompt_ids = vocab, prompt_ids
+
+    def __call__(self, prompt, add_special_tokens=True, return_tensors="pt"):
+        return {"input_ids": torch.tensor([self.prompt_ids])}
+
+    def convert_tokens_to_ids(self, tok):
+        assert tok == "<|speech_end|>"
+        return self.vocab.speech_end_id
+
+    def batch_decode(self, ids, skip_special_tokens=True):
+        lut = self.vocab.id_to_code()
+        return [f"<|s_{lut[int(i)]}|>" if lut[int(i)] >= 0 else f"<|tok_{int(i)}|>" for i in ids]
+
+
+def synth_fixture(name: str, manifest: dict) -> None:
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "shims"))
+    sys.path.insert(0, "/root/reference")
+    from tts.core.codec import decoding as ref_decoding
+    from tts.inference import inferencing as ref_inferencing
+
+    lm_arch_name, lm_seed, codec_name, codec_seed, cases = SYNTH_CASES[name]
+    arch = configs.LM_ARCHS[lm_arch_name]
+    carch = configs.CODEC_ARCHS[codec_name]
+    vocab = configs.vocab_for(arch)
+    t0 = time.time()
+    model = hf_model(arch, synth.lm_weights_cpu(arch, lm_seed))
+    cw = synth.codec_weights_cpu(carch, codec_seed)
+    with tempfile.TemporaryDirectory() as td:
+        with open(os.path.join(td, "model_config.json"), "w") as f:
+            json.dump(carch.to_json_dict(), f)
+        ck = os.path.join(td, "codec.pt")
+        torch.save({"model": {"generator." + k: v for k, v in cw.items()}}, ck)
+        dec = ref_decoding.create(ck, device="cpu")  # (the reference's strict checkpoint load)
+    rec = dict(prompt_ids=[], prompt_lens=[], speech_ids=[], speech_lens=[], settings=[], wav=[], wav_lens=[])
+    stats = []
+    for utt, n_text, n_codes, new, min_new, rep in cases:
+        prompt = synth.synthetic_prompt(vocab, utt, n_text, n_codes)
+        lut = vocab.id_to_code()
+        speech_ids = [int(lut[i]) for i in prompt[len(prompt) - n_codes:]] if n_codes else []
+        st = ref_inferencing.InferenceSettings(temperature=0.0, max_tokens=len(prompt) + new, min_tokens=min_new,
+                                               repetition_penalty=rep)
+        wav, _ = ref_inferencing._synthesize_audio(model=model, tokenizer=_IdTokenizer(vocab, prompt),
+                                                   audio_decoder=dec, speech_ids=speech_ids, prompt="",
+                                                   model_device=torch.device("cpu"), inference_settings=st,
+                                                   use_vllm=False)
+        w = wav[0].numpy().astype(np.float32)
+        stats.append(dict(utt=utt, P=len(prompt), n_prompt_codes=n_codes, L=int(w.size), rms=float(np.sqrt(np.mean(w ** 2)))))
+        rec["prompt_ids"] += prompt
+        rec["prompt_lens"].append(len(prompt))
+        rec["speech_ids"] += speech_ids
+        rec["speech_lens"].append(len(speech_ids))
+        rec["settings"].append([new, min_new, rep])
+        rec["wav"].append(w)
+        rec["wav_lens"].append(int(w.size))
+    rec["wav"] = np.concatenate(rec["wav"])
+    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), lm_arch=lm_arch_name, lm_seed=lm_seed,
+                        codec_arch=codec_name, codec_seed=codec_seed, **{k: np.asarray(v) for k, v in rec.items()})
+    manifest[name] = dict(kind="synthesize_audio", lm_arch=lm_arch_name, codec_arch=codec_name,
+                          generator="reference tts.inference.inferencing._synthesize_audio (transformers generate, "
+                          "reference decoding.create + Decoder, oracle/shims incl. lightning/absl import shims)",
                           cases=stats, seconds=round(time.time() - t0, 1))
     print(name, json.dumps(stats))
 
@@ -180,9 +355,11 @@ def main():
     mpath = os.path.join(GOLDEN, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     torch.manual_seed(0)
-    names = args.only or (list(LM_CASES) + list(CODEC_CASES))
+    names = args.only or (list(LM_CASES) + list(CHAIN_CASES) + list(SYNTH_CASES) + list(CODEC_CASES))
     for n in names:
-        (lm_fixture if n in LM_CASES else codec_fixture)(n, manifest)
+        fn = (lm_fixture if n in LM_CASES else chain_fixture if n in CHAIN_CASES else
+              synth_fixture if n in SYNTH_CASES else codec_fixture)
+        fn(n, manifest)
         with open(mpath, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
 

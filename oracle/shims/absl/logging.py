@@ -17,3 +17,18 @@ def set_verbosity(v):
 
 def get_absl_handler():
     return _l.StreamHandler()
+
+
+class converter:  # noqa: N801  (absl.logging.converter, used by custom_logging.py:38)
+    @staticmethod
+    def get_initial_for_level(level):
+        return _l.getLevelName(level)[:1]
+
+
+# names custom_logging.py touches at import time (formatter/handler classes, level constants)
+PythonFormatter = _l.Formatter
+ABSLHandler = _l.StreamHandler
+FATAL = _l.CRITICAL
+_ABSL_LOG_FATAL = _l.CRITICAL
+_CRITICAL_PREFIX = "F"
+getLogger = _l.getLogger

@@ -38,12 +38,14 @@ def _decoder(arch_name, seed):
     if key not in _dec:
         for k in list(_dec):
             _dec.pop(k).close()
-        _dec[key] = MI355XAudioDecoder.synthetic(configs.CODEC_ARCHS[arch_name], seed=seed, max_codes=256)
+        _dec[key] = MI355XAudioDecoder.synthetic(configs.CODEC_ARCHS[arch_name], seed=seed, max_codes=1024)
     return _dec[key]
 
 
-@pytest.mark.parametrize("name", ["codec_24k", "codec_16k", "codec_48k", "codec_24k_d2"])
+@pytest.mark.parametrize("name", ["codec_24k", "codec_16k", "codec_48k", "codec_24k_d2", "codec_24k_long"])
 def test_decode_matches_reference(name):
+    """codec_24k_long is the bench's codec leg: T = 650 (11 key chunks of 64 in the codec
+    attention's online softmax, the long-T GEMM plans), 300, 130 and 65 codes."""
     z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
     dec = _decoder(str(z["arch"]), int(z["seed"]))
     co = wo = 0
@@ -104,3 +106,76 @@ def test_decode_split_from_reference_codes_format(tmp_path):
         one = dec.decode(torch.tensor(u))[0].numpy()
         assert np.array_equal(wav[index[i]:index[i] + one.shape[0]], one)
     dec.close()
+
+
+def test_ragged_batch_up_to_650_codes():
+    """32 ragged utterances up to the bench's 650 codes in one decode_batch call: each equals
+    its own single decode bit for bit, and the 650-code one equals the reference waveform."""
+    z = np.load(os.path.join(GOLDEN, "codec_24k_long.npz"))
+    dec = _decoder(str(z["arch"]), int(z["seed"]))
+    T0, L0 = int(z["lens"][0]), int(z["wav_lens"][0])
+    ref650 = z["codes"][:T0]
+    rng = np.random.default_rng(32)
+    lens = [int(x) for x in rng.integers(1, 651, size=31)]
+    utts = [ref650] + [rng.integers(0, 65536, size=n) for n in lens]
+    batch = dec.decode_batch(utts)
+    _close(batch[0], z["wav"][:L0])
+    for i in (0, 1, 7, 19, 31):
+        single = dec.decode(torch.tensor(utts[i]))[0].numpy()
+        assert np.array_equal(single, batch[i]), i
+    for i, u in enumerate(utts):
+        assert batch[i].shape[0] == len(u) * 480
+
+
+def _write_codec_dir(tmp_path, arch, weights, fmt):
+    import json as _json
+
+    d = tmp_path / f"{arch.name}_{fmt}"
+    d.mkdir()
+    cfg = arch.to_json_dict()
+    if arch.depth != 12:
+        cfg["depth"] = arch.depth  # reduced-depth test variant (tts_amd extension key)
+    (d / "model_config.json").write_text(_json.dumps(cfg))
+    if fmt == "model":  # Decoder.load_from_checkpoint's strict branch: {"model": {"generator.<Decoder key>"}}
+        ck = {"model": {"generator." + k: v for k, v in weights.items()}}
+    else:  # xcodec2 release layout: {"state_dict": {"generator.<Generator key>", "fc_post_a.*"}}
+        sd = {}
+        for k, v in weights.items():
+            if k.startswith("decoder."):
+                sd["generator." + k[len("decoder."):]] = v
+            elif k.startswith("fc_post_a."):
+                sd[k] = v
+        ck = {"state_dict": sd}
+    torch.save(ck, d / "codec.pt")
+    return str(d / "codec.pt")
+
+
+@pytest.mark.parametrize("name,fmt", [("codec_24k_d2", "model"), ("codec_16k", "state_dict")])
+def test_create_from_both_checkpoint_layouts(tmp_path, name, fmt):
+    """codec.create (decoding.create + Decoder.load_from_checkpoint, decoder.py:91-119) on
+    both on-disk layouts — incl. the upsampler's weight_g / weight_v pair, folded at load —
+    reproduces the reference waveforms; a missing key raises as load_state_dict(strict)."""
+    from tts_amd import codec, configs, synth
+
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    arch = configs.CODEC_ARCHS[str(z["arch"])]
+    w = synth.codec_weights_cpu(arch, int(z["seed"]))
+    path = _write_codec_dir(tmp_path, arch, w, fmt)
+    dec = codec.create(path, device="cuda:0", max_codes=128)
+    assert dec.sample_rate == arch.sample_rate and dec.token_rate == 50
+    T, L = int(z["lens"][0]), int(z["wav_lens"][0])
+    wav = dec.decode(torch.tensor(z["codes"][:T]))
+    _close(wav[0].numpy(), z["wav"][:L])
+    dec.close()
+    # strict: a checkpoint without fc_post_a.bias is rejected before anything is uploaded
+    import shutil
+
+    d2 = tmp_path / "bad"
+    d2.mkdir()
+    shutil.copy(os.path.join(os.path.dirname(path), "model_config.json"), d2 / "model_config.json")
+    src = torch.load(path, weights_only=True)
+    top = "model" if fmt == "model" else "state_dict"
+    src[top] = {k: v for k, v in src[top].items() if not k.endswith("fc_post_a.bias")}
+    torch.save(src, d2 / "codec.pt")
+    with pytest.raises(RuntimeError, match="missing keys"):
+        codec.create(str(d2 / "codec.pt"), device=0, max_codes=16)

@@ -82,7 +82,11 @@ def test_greedy_ids_match_reference(name):
     """Free-running greedy ids equal the reference's up to its first near-tie step (all of
     the sequence for every case without one), and teacher-forced on the reference's own
     sequence the engine picks the reference's token at every step whose margin clears
-    MARGIN_TOL."""
+    MARGIN_TOL.  For the small configs that is the whole sequence.  On random TTS-1 weights
+    (lm_tts1) bf16 ties and near-ties occur from step 1 (V = 193,856, logits quantised to
+    bf16), so this case is NOT decisive; the decisive full-vocabulary bar (500 ids, no
+    margin escape) is tests/test_gpu_chain.py, and the raw TTS-1 logits are compared with
+    transformers directly in test_tts1_teacher_forced_logits_vs_transformers."""
     arch, seed, cases = _cases(name)
     m = _model(arch, seed)
     for c in cases:
@@ -319,3 +323,35 @@ def test_tts1_max_dims_logits_vs_oracle(rows):
         k = next((i for i, x in enumerate(margins) if x < 2 * 0.5 + 0.125), len(ref_new))
         assert new[r][:k] == ref_new[:k], (r, k)
     m.close()
+
+
+def test_tts1_teacher_forced_logits_vs_transformers():
+    """The engine's bf16 logits at TTS-1 dims (16 layers, V = 193,856) against transformers'
+    own teacher-forced logits (tests/golden/lm_tts1.npz tf_idx / tf_val: HF's top-32 and 32
+    fixed random ids at every generated position of both cases).  Bar: the deviation two
+    valid implementations show here — transformers vs the CPU oracle measured max 0.44 /
+    mean 0.078 (manifest tf_oracle_*), from ulp-level bf16 differences (CPU flash-attention
+    internals) that the random network amplifies to ~0.5 % of the hidden state per layer
+     — with a 2x allowance: max <= 1.0, mean <= 0.16.  The argmax agrees
+    wherever HF's top-2 margin exceeds twice the max deviation."""
+    arch, seed, cases = _cases("lm_tts1")
+    m = _model(arch, seed)
+    z = np.load(os.path.join(GOLDEN, "lm_tts1.npz"))
+    idx, val = torch.from_numpy(z["tf_idx"]).long(), torch.from_numpy(z["tf_val"])
+    off = 0
+    devs = []
+    for c in cases:
+        seq = c["prompt"] + c["hf_new"]
+        n = len(c["hf_new"])
+        lg = m.score([seq[:-1]], n)[0]  # logits predicting each generated token
+        got = torch.gather(lg, 1, idx[off:off + n])
+        d = (got - val[off:off + n]).abs()
+        devs.append(d)
+        for i in range(n):
+            top2 = torch.topk(val[off + i], 2).values  # (top-32 first: HF's own top-2)
+            if float(top2[0] - top2[1]) > 2.0:
+                assert int(idx[off + i][int(torch.argmax(got[i]))]) == int(idx[off + i][0]), i
+        off += n
+    d = torch.cat(devs)
+    assert d.max().item() <= 1.0, d.max().item()
+    assert d.mean().item() <= 0.16, d.mean().item()

@@ -72,3 +72,54 @@ def test_vllm_shaped_llm_and_http_app():
         assert client.post("/generate", json={"prompt_token_ids": [], "max_tokens": 3}).status_code == 400
     b.close()
     m.close()
+
+
+def test_sampled_requests_draw_their_own_streams():
+    """Sampling through the batcher: identical prompts submitted without a seed
+    draw different streams (each request has its own key, the same for its first token and
+    its decode steps); the same explicit per-request seed reproduces the same tokens whatever
+    slot the request lands in and whatever the batch holds."""
+    from tts_amd.serving import ContinuousBatcher
+
+    m, z = _model()
+    p = z["prompt_ids"][:int(z["prompt_lens"][0])].tolist()
+    b = ContinuousBatcher(m, n_slots=3, do_sample=True, temperature=1.0, top_k=50, repetition_penalty=1.1, chunk=4)
+    outs = b.generate([p] * 4, 24)
+    assert len({tuple(o) for o in outs}) > 1  # 24 draws at T = 1 from top-50: equal streams would tie
+    seeded = b.generate([p] * 4, 24, seed=1234)
+    assert all(o == seeded[0] for o in seeded)
+    alone = ContinuousBatcher(m, n_slots=1, do_sample=True, temperature=1.0, top_k=50, repetition_penalty=1.1,
+                              chunk=7).generate([p], 24, seed=1234)[0]
+    assert alone == seeded[0]
+    m.close()
+
+
+def test_engine_error_fails_every_request_and_health():
+    """A failing engine call inside the serving loop fails all active and queued requests
+    (no hang) and marks the batcher dead."""
+    from fastapi.testclient import TestClient
+
+    from tts_amd.serving import ContinuousBatcher, create_app
+
+    m, z = _model()
+    p = z["prompt_ids"][:int(z["prompt_lens"][0])].tolist()
+    b = ContinuousBatcher(m, n_slots=2, repetition_penalty=1.1, chunk=4)
+    orig = b.run_once
+
+    def boom():
+        raise RuntimeError("injected engine failure")
+
+    b.run_once = boom
+    futs = [b.submit(p, 8) for _ in range(3)]
+    b.start()
+    for f in futs:
+        with pytest.raises(RuntimeError, match="injected"):
+            f.result(timeout=30)
+    assert b.error is not None
+    with pytest.raises(RuntimeError):
+        b.submit(p, 8).result(timeout=5)
+    with TestClient(create_app(b)) as client:
+        assert client.get("/health").status_code == 503
+    b.run_once = orig
+    b.close()
+    m.close()

@@ -3,6 +3,7 @@
 // message, never an exception across the ABI.
 #include <stdlib.h>
 
+#include <memory>
 #include <string>
 
 #include "../../include/tts_mi355x.h"
@@ -59,14 +60,14 @@ tts_status tts_engine_create(int32_t device, tts_engine** out) {
     HIP_CHECK(hipGetDeviceCount(&n));
     TTS_REQUIRE(device >= 0 && device < n, "device index out of range");
     HIP_CHECK(hipSetDevice(device));
-    Engine* e = new Engine();
+    std::unique_ptr<Engine> e(new Engine());  // freed if a HIP call below throws
     e->device = device;
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     e->num_cu = prop.multiProcessorCount;
     HIP_CHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     for (auto& v : e->ev) HIP_CHECK(hipEventCreate(&v));
-    *out = reinterpret_cast<tts_engine*>(e);
+    *out = reinterpret_cast<tts_engine*>(e.release());
   });
 }
 
@@ -92,7 +93,8 @@ tts_status tts_generate(tts_engine* e, const tts_gen_params* p, const int32_t* p
                         const int32_t* prompt_lens, int32_t batch, int32_t* out_ids,
                         int32_t out_stride, int32_t* out_lens, void* stream) {
   return guarded([&] {
-    TTS_REQUIRE(e && out_ids && out_lens, "null argument");
+    TTS_REQUIRE(e && p && prompt_ids && prompt_lens && out_ids && out_lens, "null argument");
+    TTS_REQUIRE(batch >= 1, "batch must be >= 1");
     Engine* E = reinterpret_cast<Engine*>(e);
     HIP_CHECK(hipSetDevice(E->device));
     lm_generate(E, p, prompt_ids, prompt_lens, batch, out_ids, out_stride, out_lens,
@@ -143,7 +145,17 @@ tts_status tts_slots_add(tts_engine* e, int32_t slot, const int32_t* prompt_ids,
     TTS_REQUIRE(e && prompt_ids, "null argument");
     Engine* E = reinterpret_cast<Engine*>(e);
     HIP_CHECK(hipSetDevice(E->device));
-    lm_slots_add(E, slot, prompt_ids, prompt_len, max_new_tokens);
+    lm_slots_add(E, slot, prompt_ids, prompt_len, max_new_tokens, nullptr);
+  });
+}
+
+tts_status tts_slots_add_seeded(tts_engine* e, int32_t slot, const int32_t* prompt_ids, int32_t prompt_len,
+                         int32_t max_new_tokens, uint64_t seed) {
+  return guarded([&] {
+    TTS_REQUIRE(e && prompt_ids, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_slots_add(E, slot, prompt_ids, prompt_len, max_new_tokens, &seed);
   });
 }
 

@@ -91,6 +91,7 @@ struct LmWork {
   DevBuf logits;                                    // scoring output (bf16)
   DevBuf row_slot, row_pos, row_idx;                // prefill row descriptors
   DevBuf st_int;                                    // step-state ints
+  DevBuf row_seed;                                  // [B] u64 sampling key of each row (graph-invariant)
   DevBuf seen;                                      // [B][V/32]
   DevBuf out_ids;                                   // [B][max_new]
   int out_cap = 0;
@@ -103,7 +104,6 @@ struct LmWork {
   // sampling parameters baked into the captured step (kernel arguments)
   int graph_sample = -1, graph_top_k = -1;
   float graph_temp = -1.f, graph_top_p = -1.f;
-  unsigned long long graph_seed = 0;
   float graph_freq = 0.f;
   int* h_active = nullptr;  // pinned host copy of n_active (ring of 2)
 };
@@ -133,6 +133,7 @@ struct Engine {
     bool open = false;
     int S = 0;
     tts_gen_params gp{};
+    unsigned long long next_req = 0;  // default per-request sampling keys
     std::vector<int> busy;  // 1 while a sequence owns the slot (until released)
     hipStream_t s = nullptr;
   } slots;
@@ -150,7 +151,7 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
 int lm_gen_continue(Engine* e, int n_steps);
 void lm_gen_read(Engine* e, int32_t* out_ids, int out_stride, int32_t* out_lens);
 void lm_slots_open(Engine* e, const tts_gen_params* p, int S, hipStream_t s);
-void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_new);
+void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_new, const uint64_t* seed);
 int lm_slots_step(Engine* e, int n_steps);
 void lm_slots_read(Engine* e, int slot, int32_t* out_ids, int cap, int32_t* n_out, int32_t* finished);
 void lm_slots_release(Engine* e, int slot);

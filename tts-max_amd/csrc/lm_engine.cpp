@@ -54,8 +54,16 @@ void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& s
       src = staging.as<float>();
     }
     launch_f32_to_bf16(src, dst, n, s);
+  } else if (d.dtype == TTS_DT_F16) {
+    const void* src = d.data;
+    if (!d.on_device) {
+      if (staging.bytes < (size_t)n * 2) staging.alloc((size_t)n * 2);
+      HIP_CHECK(hipMemcpyAsync(staging.p, d.data, n * 2, hipMemcpyHostToDevice, s));
+      src = staging.p;
+    }
+    launch_f16_to_bf16(src, dst, n, s);
   } else {
-    throw Error(TTS_E_UNSUPPORTED, std::string("tensor ") + d.name + ": dtype must be bf16 or f32");
+    throw Error(TTS_E_UNSUPPORTED, std::string("tensor ") + d.name + ": dtype must be bf16, f16 or f32");
   }
 }
 
@@ -260,6 +268,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.row_pos.alloc((size_t)R * 4);
   w.row_idx.alloc((size_t)R * 4);
   w.st_int.alloc((size_t)B * 8 * 4 + 64);
+  w.row_seed.alloc((size_t)B * 8);
   w.seen.alloc((size_t)B * (V / 32 + 1) * 4);
   w.out_cap = S;
   w.out_ids.alloc((size_t)B * S * 4);
@@ -472,6 +481,7 @@ struct Ctx {
     st.seen = w.seen.as<uint32_t>();
     st.seen_stride = c.vocab_size / 32 + 1;
     st.counts = nullptr;
+    st.row_seed = w.row_seed.as<unsigned long long>();
     st.out_ids = w.out_ids.as<int>();
     st.out_stride = w.out_cap;
     st.eos_id = eos;
@@ -498,7 +508,7 @@ struct Ctx {
       SampleArgs sa;
       sa.logits = w.slogits.as<float>(); sa.ldl = c.vocab_size; sa.V = c.vocab_size;
       sa.temperature = gp.temperature; sa.top_k = gp.top_k; sa.top_p = gp.top_p;
-      sa.seed = gp.seed; sa.step = st.gen_count; sa.done = st.done;
+      sa.seed = gp.seed; sa.row_seed = st.row_seed; sa.step = st.gen_count; sa.done = st.done;
       sa.part_val = ex.part_val; sa.nparts = p.grid; sa.part_stride = LOGITS_MAX_PARTS;
       sa.out_part_val = ex.part_val; sa.out_part_idx = ex.part_idx;
       launch_sample(sa, B, s);
@@ -538,7 +548,8 @@ static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, 
 
 // The decode step (all layers + lm_head + pick + finalize over B rows) captured once into a
 // hipGraph.  The graph bakes in B, the penalty, eos/min_new and the sampling parameters
-// (kernel arguments): recaptured when any of them changes.
+// (kernel arguments): recaptured when any of them changes.  The sampling keys are per-row
+// device values (w.row_seed), so a new seed needs no recapture.
 static void ensure_step_graph(Engine* e, int B, const StepState& st, const tts_gen_params& gp) {
   LmWork& W = e->w;
   const tts_gen_params* p = &gp;
@@ -546,7 +557,7 @@ static void ensure_step_graph(Engine* e, int B, const StepState& st, const tts_g
   const bool smp_changed =
       W.graph_sample != p->do_sample ||
       (p->do_sample && (W.graph_temp != p->temperature || W.graph_top_k != p->top_k ||
-                        W.graph_top_p != p->top_p || W.graph_seed != p->seed)) ||
+                        W.graph_top_p != p->top_p)) ||
       W.graph_freq != p->frequency_penalty;
   if (W.graph && (W.graph_batch != B || W.graph_pen != pen || W.graph_eos != p->eos_token_id ||
                   W.graph_min_new != p->min_new_tokens || smp_changed)) {
@@ -576,7 +587,6 @@ static void ensure_step_graph(Engine* e, int B, const StepState& st, const tts_g
   W.graph_temp = p->temperature;
   W.graph_top_k = p->top_k;
   W.graph_top_p = p->top_p;
-  W.graph_seed = p->seed;
   W.graph_freq = p->frequency_penalty;
 }
 
@@ -629,6 +639,12 @@ void lm_gen_begin(Engine* e, const tts_gen_params* p, const int32_t* ids, const 
   HIP_CHECK(hipMemcpyAsync(e->w.st_int.p, st_host.data(), st_host.size() * 4,
                            hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(e->w.seen.p, seen.data(), seen.size() * 4, hipMemcpyHostToDevice, s));
+  {  // row b draws with key seed + GOLD * (b << 32)  (rng_uniform(key, 0, step))
+    std::vector<unsigned long long> rs(B);
+    for (int b = 0; b < B; ++b) rs[b] = p->seed + 0x9E3779B97F4A7C15ull * ((unsigned long long)b << 32);
+    HIP_CHECK(hipMemcpyAsync(e->w.row_seed.p, rs.data(), B * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));  // (rs is a stack buffer)
+  }
   // rows' slots are 0..B-1 in the decode phase: prepare a persistent identity map
   HIP_CHECK(hipEventRecord(e->ev[2], s));
 
@@ -789,6 +805,7 @@ void lm_slots_open(Engine* e, const tts_gen_params* p, int S, hipStream_t s) {
   Z.S = S;
   Z.gp = *p;
   Z.busy.assign(S, 0);
+  Z.next_req = 0;
   Z.s = s;
   const int V = e->lm.cfg.vocab_size;
   // every row idle: done = 1, n_active = 0, no EOS mask
@@ -804,7 +821,9 @@ void lm_slots_open(Engine* e, const tts_gen_params* p, int S, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
-void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_new) {
+// seed: the request's sampling key (vLLM SamplingParams.seed); nullptr = the batch seed
+// mixed with a request counter, so every request draws its own stream
+void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_new, const uint64_t* seed) {
   Engine::Slots& Z = e->slots;
   TTS_REQUIRE(Z.open, "no slot batch open (tts_slots_open)");
   TTS_REQUIRE(slot >= 0 && slot < Z.S && !Z.busy[slot], "slot out of range or busy");
@@ -831,6 +850,11 @@ void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_n
   int* base = e->w.st_int.as<int>();
   for (int k = 0; k < 6; ++k)  // tokens, pos, gen_count, limit, done, eos_mask
     HIP_CHECK(hipMemcpyAsync(base + k * S + slot, &row[k], 4, hipMemcpyHostToDevice, s));
+  // the row's sampling key: the same for its first token (drawn below as a batch of 1) and
+  // for every decode step (row = slot)
+  const unsigned long long key =
+      seed ? (unsigned long long)*seed : Z.gp.seed + 0x9E3779B97F4A7C15ull * ((++Z.next_req) << 32);
+  HIP_CHECK(hipMemcpyAsync(st.row_seed + slot, &key, 8, hipMemcpyHostToDevice, s));
   int act = 0;
   HIP_CHECK(hipMemcpyAsync(&act, st.n_active, 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -846,7 +870,7 @@ void lm_slots_add(Engine* e, int slot, const int32_t* prompt, int len, int max_n
                      c.hidden_size, s);
   StepState one = st;  // the slot's row as a batch of 1
   one.tokens += slot; one.pos += slot; one.gen_count += slot; one.limit += slot;
-  one.done += slot; one.eos_mask += slot;
+  one.done += slot; one.eos_mask += slot; one.row_seed += slot;
   one.seen += (size_t)slot * stride;
   one.out_ids += (size_t)slot * one.out_stride;
   if (one.counts) one.counts += (size_t)slot * stride * 32;

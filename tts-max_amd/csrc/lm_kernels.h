@@ -159,6 +159,7 @@ void launch_gather_rows(const bf16_t* x, int ld, const int* rows, bf16_t* y, int
 void launch_synth_fill(void* dst, int dtype, long long n, unsigned long long seed, float scale,
                        hipStream_t s);
 void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s);
+void launch_f16_to_bf16(const void* x, bf16_t* y, long long n, hipStream_t s);  // x: _Float16
 // K-sliced GEMM combine: v = bf16(sum_c part[c][m][n]);  resid ? resid += v : out = v
 void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
                            bf16_t* resid, int ldo, hipStream_t s);
@@ -185,6 +186,7 @@ struct SampleArgs {
   int top_k = 50;                 // 1 .. 1024
   float top_p = 1.f;
   unsigned long long seed = 0;
+  const unsigned long long* row_seed = nullptr;  // per-row keys (seed, row ignored) or nullptr
   const int* step = nullptr;      // per-row draw counter (generated count), or step0
   int step0 = 0;
   const int* done = nullptr;      // rows already stopped (skipped)
@@ -212,6 +214,7 @@ struct StepState {
   int out_stride;
   int* n_active;      // [1]
   uint16_t* counts;   // [B][V] new-token counts (frequency penalty) or nullptr
+  unsigned long long* row_seed;  // [B] sampling key of each row
   int eos_id;
   int min_new;
 };

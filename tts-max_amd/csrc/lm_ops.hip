@@ -332,4 +332,19 @@ void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s) {
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid), dim3(256), 0, s, x, y, n);
 }
 
+// fp16 checkpoints (the serving CLI loads the LM with torch_dtype=float16,
+// tools/serving/inference.py:103-107): f16 -> f32 is exact, then one RNE rounding to bf16
+// (exact for weights that came from the bf16 training checkpoint).
+__global__ void f16_to_bf16_kernel(const _Float16* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] = f2bf((float)x[i]);
+}
+
+void launch_f16_to_bf16(const void* x, bf16_t* y, long long n, hipStream_t s) {
+  long long g = (n + 255) / 256;
+  int grid = (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+  hipLaunchKernelGGL(f16_to_bf16_kernel, dim3(grid), dim3(256), 0, s, (const _Float16*)x, y, n);
+}
+
 }  // namespace tts

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
     float z2 = 0.f;
     for (int i = 0; i < nkeep; ++i) z2 += expf(okey_inv((uint32_t)(cand[i] >> 32)) - mx);
     const int step = a.step ? a.step[b] : a.step0;
-    const float u = rng_uniform(a.seed, b, step) * z2;
+    const float u = (a.row_seed ? rng_uniform(a.row_seed[b], 0, step) : rng_uniform(a.seed, b, step)) * z2;
     float acc = 0.f;
     int pick = nkeep - 1;
     for (int i = 0; i < nkeep; ++i) {

@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "tts_generate_read",
     "tts_slots_open",
     "tts_slots_add",
+    "tts_slots_add_seeded",
     "tts_slots_step",
     "tts_slots_read",
     "tts_slots_release",
@@ -159,6 +160,7 @@ def load_library() -> ctypes.CDLL:
         "tts_generate_read": (I32, [P, pi32, I32, pi32]),
         "tts_slots_open": (I32, [P, ctypes.POINTER(GenParams), I32, P]),
         "tts_slots_add": (I32, [P, I32, pi32, I32, I32]),
+        "tts_slots_add_seeded": (I32, [P, I32, pi32, I32, I32, ctypes.c_uint64]),
         "tts_slots_step": (I32, [P, I32, pi32]),
         "tts_slots_read": (I32, [P, I32, pi32, I32, pi32, pi32]),
         "tts_slots_release": (I32, [P, I32]),

@@ -36,13 +36,30 @@ class AudioDecoderInterface(metaclass=abc.ABCMeta):
         raise NotImplementedError
 
 
-def load_codec_checkpoint(path: str) -> dict[str, torch.Tensor]:
-    """Decoder.load_from_checkpoint key mapping (tts/core/codec/decoder.py:91-119):
-    {"model": {"generator.*"}} (strict) or xcodec2 {"state_dict": {"generator.*", "fc_post_a.*"}}.
-    Loaded with weights_only=True (no pickled code is executed)."""
+def expected_codec_keys(arch: configs.CodecArch) -> set[str]:
+    """The reference Decoder's state-dict keys for `arch` (tts/core/codec/decoder.py:14-67;
+    the synthetic generator emits exactly these, pinned by load_state_dict(strict=True) in
+    oracle/make_golden.py)."""
+    keys = {name for name, *_ in synth.codec_tensor_specs(arch)}
+    keys |= {"decoder.head.istft.window", "decoder.quantizer.project_in.weight", "decoder.quantizer.project_in.bias"}
+    return keys
+
+
+def load_codec_checkpoint(path: str, arch: configs.CodecArch | None = None) -> dict[str, torch.Tensor]:
+    """Decoder.load_from_checkpoint (tts/core/codec/decoder.py:91-119), loaded with
+    weights_only=True (no pickled code is executed):
+
+    * {"model": {"generator.<Decoder key>"}}: the prefix stripped, then load_state_dict(strict)
+      into the whole Decoder — missing or unexpected keys raise, as there;
+    * xcodec2 {"state_dict": {"generator.<Generator key>", "fc_post_a.*"}}: the Generator and
+      fc_post_a loaded strictly; the reference leaves an upsampler (none in xcodec2) at its
+      random init, which cannot be reproduced, so a config with upsampling raises here.
+
+    ConvTranspose weight-norm pairs (weight_g, weight_v) are folded by the engine at load."""
     ckpt = torch.load(path, map_location="cpu", weights_only=True)
     out: dict[str, torch.Tensor] = {}
-    if "state_dict" in ckpt:
+    xcodec2 = "state_dict" in ckpt
+    if xcodec2:
         for k, v in ckpt["state_dict"].items():
             if k.startswith("generator."):
                 out["decoder." + k[len("generator."):]] = v
@@ -52,6 +69,17 @@ def load_codec_checkpoint(path: str) -> dict[str, torch.Tensor]:
         for k, v in ckpt["model"].items():
             if k.startswith("generator."):
                 out[k[len("generator."):]] = v
+    if arch is not None:
+        want = expected_codec_keys(arch)
+        if xcodec2:
+            if arch.upsample_factors:
+                raise ValueError("xcodec2 state_dict checkpoints carry no upsampler weights; "
+                                 f"config {arch.name} has upsample factors {arch.upsample_factors}")
+            want = {k for k in want if k.startswith(("decoder.", "fc_post_a."))}
+        missing, unexpected = sorted(want - set(out)), sorted(set(out) - want)
+        if missing or unexpected:
+            raise RuntimeError(f"Error(s) in loading state_dict for Decoder: missing keys {missing[:8]}, "
+                               f"unexpected keys {unexpected[:8]}")
     return {k: v.float().contiguous() for k, v in out.items() if torch.is_tensor(v)}
 
 
@@ -156,4 +184,4 @@ def create(model_path: str, device: torch.device | str | int | None = 0, max_cod
         device = device.index or 0
     elif isinstance(device, str):
         device = int(device.split(":")[1]) if ":" in device else 0
-    return MI355XAudioDecoder(arch, load_codec_checkpoint(model_path), device=device or 0, max_codes=max_codes)
+    return MI355XAudioDecoder(arch, load_codec_checkpoint(model_path, arch), device=device or 0, max_codes=max_codes)

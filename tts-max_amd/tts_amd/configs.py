@@ -127,13 +127,14 @@ class CodecArch:
     @staticmethod
     def from_json(path: str | os.PathLike, name: str = "json") -> "CodecArch":
         """DecoderConfig.from_json; `model_type` is optional here (the shipped
-        example/codec/model_config.json lacks it, which makes the reference raise)."""
+        example/codec/model_config.json lacks it, which makes the reference raise).  An
+        optional `depth` key (not a reference key) selects the reduced-depth test variants."""
         with open(path) as f:
             c = json.load(f)
         return CodecArch(name=name, sample_rate=c["sample_rate"], token_rate=c["token_rate"],
                          hop_length=c["hop_length"], upsample_factors=tuple(c.get("upsample_factors") or ()),
                          kernel_sizes=tuple(c.get("kernel_sizes") or ()),
-                         model_type=c.get("model_type", "xcodec2"))
+                         model_type=c.get("model_type", "xcodec2"), depth=int(c.get("depth", 12)))
 
     def to_json_dict(self) -> dict:
         return dict(model_type=self.model_type, sample_rate=self.sample_rate, token_rate=self.token_rate,

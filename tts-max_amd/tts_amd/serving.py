@@ -47,6 +47,7 @@ class _Req:
     prompt: list[int]
     max_new: int
     future: Future
+    seed: int | None = None  # the request's own sampling key (vLLM SamplingParams.seed)
 
 
 class ContinuousBatcher:
@@ -71,34 +72,73 @@ class ContinuousBatcher:
         self._opened = False
         self._thread: threading.Thread | None = None
         self._buf = np.zeros(lm.max_seq_len, dtype=np.int32)
+        self.error: BaseException | None = None  # set when the engine loop failed (batcher dead)
 
     # ------------------------------------------------------------------ requests -------
-    def submit(self, prompt_ids: Sequence[int], max_new_tokens: int) -> Future:
+    def submit(self, prompt_ids: Sequence[int], max_new_tokens: int, seed: int | None = None) -> Future:
+        """Queues a request.  `seed` fixes the request's sampling stream (vLLM per-request
+        seed); None draws a fresh stream per request from the batcher's seed."""
         fut: Future = Future()
+        if self.error is not None:
+            fut.set_exception(RuntimeError(f"batcher stopped after an engine error: {self.error}"))
+            return fut
         with self._lock:
-            self._queue.append(_Req(list(map(int, prompt_ids)), int(max_new_tokens), fut))
+            self._queue.append(_Req(list(map(int, prompt_ids)), int(max_new_tokens), fut,
+                                    None if seed is None else int(seed) & (2**64 - 1)))
         self._wake.set()
         return fut
 
-    def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int | Sequence[int]) -> list[list[int]]:
+    def busy(self) -> bool:
+        with self._lock:
+            return bool(self._queue) or any(r is not None for r in self._slot_req)
+
+    def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int | Sequence[int],
+                 seed: int | None = None) -> list[list[int]]:
         """Blocking: all prompts through the continuous batch, results in order."""
         if isinstance(max_new_tokens, int):
             max_new_tokens = [max_new_tokens] * len(prompts)
-        futs = [self.submit(p, n) for p, n in zip(prompts, max_new_tokens)]
+        futs = [self.submit(p, n, seed) for p, n in zip(prompts, max_new_tokens)]
         if self._thread is None:  # no background loop: drive it here
             while not all(f.done() for f in futs):
-                self.run_once()
+                self._run_guarded()
         return [f.result() for f in futs]
 
     # ------------------------------------------------------------------ engine loop ----
     def _open(self):
-        if not self._opened:
+        if not self._opened or self.lm._slot_batcher is not self:
             _lib.check(self.lm._lib.tts_slots_open(self.lm._h, ctypes.byref(self._p), self.S, None))
+            self.lm._slot_batcher = self
             self._opened = True
+
+    def _fail_all(self, ex: BaseException) -> None:
+        """An engine error ends the batcher: every active and queued request fails with it
+        (no future is left pending), and later submissions fail at once."""
+        self.error = ex
+        with self._lock:
+            reqs = [r for r in self._slot_req if r is not None] + self._queue
+            self._slot_req = [None] * self.S
+            self._queue = []
+        for r in reqs:
+            if not r.future.done():
+                r.future.set_exception(ex)
+        if self.lm._slot_batcher is self:
+            self.lm._slot_batcher = None
+        self._opened = False
+
+    def _run_guarded(self) -> int:
+        try:
+            return self.run_once()
+        except Exception as ex:  # noqa: BLE001 (TtsError and anything else: fail loudly, never hang)
+            self._fail_all(ex)
+            return 0
 
     def run_once(self) -> int:
         """Admit queued requests into free slots, run one chunk of decode steps, retire the
         stopped sequences.  Returns the number of rows still generating."""
+        with self.lm.lock:
+            return self._run_once_locked()
+
+    def _run_once_locked(self) -> int:
         self._open()
         h, L = self.lm._h, self.lm._lib
         pi32 = ctypes.POINTER(ctypes.c_int32)
@@ -108,8 +148,12 @@ class ContinuousBatcher:
                     r = self._queue.pop(0)
                     arr = np.ascontiguousarray(np.asarray(r.prompt, dtype=np.int32))
                     try:
-                        _lib.check(L.tts_slots_add(h, s, arr.ctypes.data_as(pi32), len(arr), r.max_new))
-                    except Exception as ex:  # bad request: fail it, keep serving
+                        if r.seed is None:
+                            _lib.check(L.tts_slots_add(h, s, arr.ctypes.data_as(pi32), len(arr), r.max_new))
+                        else:
+                            _lib.check(L.tts_slots_add_seeded(h, s, arr.ctypes.data_as(pi32), len(arr), r.max_new,
+                                                              r.seed))
+                    except _lib.TtsError as ex:  # bad request: fail it, keep serving
                         r.future.set_exception(ex)
                         continue
                     self._slot_req[s] = r
@@ -142,7 +186,9 @@ class ContinuousBatcher:
                     self._wake.wait(0.05)
                     self._wake.clear()
                     continue
-                self.run_once()
+                self._run_guarded()
+                if self.error is not None:
+                    return
 
         self._thread = threading.Thread(target=loop, name="tts-mi355x-batcher", daemon=True)
         self._thread.start()
@@ -186,7 +232,7 @@ class LLM:
             raise NotImplementedError("full-vocabulary sampling (vLLM top_k=-1) is not built; pass top_k")
         key = (temperature, stop[0] if stop else -1, int(getattr(sp, "min_tokens", 0) or 0),
                float(getattr(sp, "repetition_penalty", 1.0) or 1.0), top_k, float(getattr(sp, "top_p", 1.0) or 1.0),
-               float(getattr(sp, "frequency_penalty", 0.0) or 0.0), getattr(sp, "seed", None))
+               float(getattr(sp, "frequency_penalty", 0.0) or 0.0))
         if key not in self._batchers:
             for b in self._batchers.values():  # one slot batch open per engine at a time
                 b._opened = False
@@ -194,7 +240,7 @@ class LLM:
             self._batchers[key] = ContinuousBatcher(
                 self.lm, self.n_slots, eos_token_id=key[1], min_new_tokens=key[2], repetition_penalty=key[3],
                 do_sample=temperature > 0, temperature=temperature or 1.0, top_k=top_k if top_k > 0 else 50,
-                top_p=key[5], frequency_penalty=key[6], seed=key[7], chunk=self.chunk)
+                top_p=key[5], frequency_penalty=key[6], seed=None, chunk=self.chunk)
         return self._batchers[key]
 
     def generate(self, prompt_token_ids: Sequence[int] | Sequence[Sequence[int]], sampling_params: Any = None,
@@ -203,7 +249,8 @@ class LLM:
         if prompts and isinstance(prompts[0], (int, np.integer)):
             prompts = [prompts]
         b = self._batcher(sampling_params)
-        outs = b.generate(prompts, int(getattr(sampling_params, "max_tokens", 16)))
+        outs = b.generate(prompts, int(getattr(sampling_params, "max_tokens", 16)),
+                          seed=getattr(sampling_params, "seed", None))
         return [RequestOutput(prompt_token_ids=list(p), outputs=[CompletionOutput(token_ids=o)])
                 for p, o in zip(prompts, outs)]
 
@@ -230,6 +277,8 @@ def create_app(batcher: ContinuousBatcher):
 
     @app.get("/health")
     async def health():
+        if batcher.error is not None:
+            raise HTTPException(status_code=503, detail=f"engine error: {batcher.error}")
         return {"ok": True}
 
     return app

@@ -20,6 +20,7 @@ import dataclasses
 import json
 import math
 import os
+import threading
 from typing import Any, Sequence
 
 import numpy as np
@@ -77,6 +78,10 @@ class MI355XSpeechLM:
         self.max_batch = max_batch
         self.max_seq_len = max_seq_len
         self._lib = _lib.load_library()
+        # one engine = one caller at a time (C ABI: not re-entrant); the continuous batcher
+        # that holds the engine's slot batch, if any (serving.ContinuousBatcher)
+        self.lock = threading.RLock()
+        self._slot_batcher = None
         h = ctypes.c_void_p()
         _lib.check(self._lib.tts_engine_create(device, ctypes.byref(h)))
         self._h = h
@@ -103,10 +108,14 @@ class MI355XSpeechLM:
 
     # ------------------------------------------------------------------ constructors ---
     @classmethod
-    def synthetic(cls, arch: configs.LmArch, seed: int = 0x5EED, device: int = 0, **kw) -> "MI355XSpeechLM":
+    def synthetic(cls, arch: configs.LmArch, seed: int = 0x5EED, device: int = 0,
+                  chain: "synth.ChainSpec | None" = None, **kw) -> "MI355XSpeechLM":
         """Random-init weights of `arch`, generated on the device (bit-identical to the
-        CPU generator the golden fixtures were made with)."""
+        CPU generator the golden fixtures were made with); `chain` overwrites the rows of
+        the decisive-parity model (synth.apply_chain)."""
         w = synth.lm_weights_device(arch, seed, torch.device("cuda", device))
+        if chain is not None:
+            synth.apply_chain(w, arch, chain)
         vocab = configs.vocab_for(arch)
         m = cls(arch, w, device=device, id_to_code=vocab.id_to_code(), **kw)
         del w
@@ -190,6 +199,25 @@ class MI355XSpeechLM:
         B = len(prompts)
         if B < 1 or B > self.max_batch:
             raise ValueError(f"batch {B} outside [1, max_batch={self.max_batch}]")
+        with self.lock:
+            self._take_from_batcher()
+            return self._generate_batch_locked(prompts, max_length, min_new_tokens, eos_token_id, do_sample,
+                                               repetition_penalty, top_p, temperature, top_k, seed,
+                                               frequency_penalty)
+
+    def _take_from_batcher(self):
+        """A one-shot generation reuses the decode rows a continuous batcher holds: refuse while
+        it serves requests, otherwise let it reopen its slot batch next time."""
+        b = self._slot_batcher
+        if b is not None:
+            if b.busy():
+                raise RuntimeError("the engine's continuous batcher is serving requests; "
+                                   "use the batcher (or another engine) for this generation")
+            self._slot_batcher = None
+
+    def _generate_batch_locked(self, prompts, max_length, min_new_tokens, eos_token_id, do_sample,
+                               repetition_penalty, top_p, temperature, top_k, seed, frequency_penalty):
+        B = len(prompts)
         lens = np.array([len(p) for p in prompts], dtype=np.int32)
         for p in prompts:
             if len(p) >= max_length:
@@ -228,6 +256,11 @@ class MI355XSpeechLM:
                                 do_sample=1 if do_sample else 0, repetition_penalty=repetition_penalty,
                                 temperature=temperature, top_p=top_p, top_k=50 if top_k is None else top_k,
                                 seed=0 if seed is None else seed)
+        with self.lock:
+            self._take_from_batcher()
+            yield from self._stream_locked(B, flat, lens, params, max_length, chunk)
+
+    def _stream_locked(self, B, flat, lens, params, max_length, chunk):
         pi32 = ctypes.POINTER(ctypes.c_int32)
         _lib.check(self._lib.tts_generate_begin(self._h, ctypes.byref(params), flat.ctypes.data_as(pi32),
                                                 lens.ctypes.data_as(pi32), B, None))
@@ -270,6 +303,11 @@ class MI355XSpeechLM:
     # ------------------------------------------------------------------ utilities ------
     def score(self, sequences: Sequence[Sequence[int]], n_last: int) -> torch.Tensor:
         """Teacher-forced bf16 logits (as fp32) of the last n_last positions: [B, n_last, V]."""
+        with self.lock:
+            self._take_from_batcher()
+            return self._score_locked(sequences, n_last)
+
+    def _score_locked(self, sequences, n_last):
         B = len(sequences)
         lens = np.array([len(s) for s in sequences], dtype=np.int32)
         flat = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32) for s in sequences]))

@@ -53,7 +53,7 @@ class StreamingSynthesizer:
                 if pending >= self.chunk or (flush and pending > 0):
                     n = min(self.chunk, pending)
                     hist = list(prompt_codes[b]) + codes[:voiced[b]]
-                    ctx = hist[len(hist) - self.left:] if self.left > 0 else []
+                    ctx = hist[max(0, len(hist) - self.left):] if self.left > 0 else []
                     wins.append(ctx + codes[voiced[b]:voiced[b] + n])
                     rows.append(b)
                     emit.append(n)

@@ -12,6 +12,7 @@ Weight names are the reference state-dict keys: HF Llama keys for the SpeechLM a
 
 from __future__ import annotations
 
+import dataclasses
 import math
 import zlib
 
@@ -109,6 +110,121 @@ def lm_weights_device(arch: configs.LmArch, seed: int, device) -> dict[str, torc
             out[name] = t
     torch.cuda.synchronize()
     return out
+
+
+# ------------------------------------------------- decisive greedy-parity model ("chain") ---
+#
+# With random weights the bf16 dataflow is chaotic at the ulp level: two valid
+# implementations (transformers on CPU, the engine) differ by ~0.5 % of the hidden state per
+# layer, so over hundreds of free-running steps some top-1/top-2 margin always falls inside
+# that noise and "bit-exact ids" cannot be shown on random weights alone.  The chain model
+# keeps every random tensor (the same numerics everywhere) and overwrites a few rows with
+# exact values so that each step's argmax is decided by a margin far above the noise AND by
+# the greedy head's semantics (repetition penalty over prompt + generated ids, the
+# min-new-tokens EOS mask, EOS stop):
+#
+# * chain tokens c_0..c_{U-1} (distinct <|s_N|> ids) and EOS get embedding rows s*H_r, r a
+#   Sylvester-Hadamard row (exactly orthogonal, exact in bf16; tied => also their lm_head rows);
+# * MLP unit j of layer 0 detects c_j (gate = up = 2^g H_{r(j)}) and writes
+#   2^q (H_{r(j+1)} + w_seen H_{r(j-lag)}) into the residual: the already-generated
+#   c_{j-lag} has the larger raw logit (x w_seen = 1.046875) but, penalised by
+#   repetition_penalty = 1.1, loses to the fresh c_{j+1} (and wins without a penalty);
+# * units j = eos_phase (mod eos_period) write 2^q (H_{r(j+1)} + 2 H_eos) instead: EOS wins
+#   unless min_new_tokens masks it.
+#
+# Every value is a signed power of two or a sum of two such values, so the construction is
+# bit-identical with numpy on the CPU and torch on the device.
+
+@dataclasses.dataclass(frozen=True)
+class ChainSpec:
+    seed: int = 0xC4A1
+    units: int = 2040            # chain tokens (Hadamard rows 1..units), EOS uses row `eos_row`
+    eos_row: int = 2047
+    emb_exp: int = -3            # embedding rows s*H, s = 2^emb_exp
+    gate_exp: int = -7           # gate/up rows 2^gate_exp * H
+    down_exp: int = -1           # down columns 2^down_exp * (H_next + w H_seen)
+    lag: int = 7
+    w_seen: float = 1.046875     # 1 + 3/64 (exact in bf16)
+    eos_period: int = 150
+    eos_phase: int = 40
+
+
+def hadamard_rows(rows, n: int) -> np.ndarray:
+    """Rows of the n x n Sylvester-Hadamard matrix: H[r][k] = (-1)^popcount(r & k)."""
+    r = np.asarray(rows, dtype=np.int64)[:, None]
+    k = np.arange(n, dtype=np.int64)[None, :]
+    x = r & k
+    par = np.zeros_like(x)
+    while np.any(x):
+        par ^= x & 1
+        x >>= 1
+    return (1 - 2 * par).astype(np.float32)
+
+
+def chain_tokens(vocab, spec: ChainSpec) -> list[int]:
+    rng = np.random.default_rng(spec.seed)
+    codes = rng.permutation(vocab.codebook_size)[: spec.units]
+    return [int(vocab.code_to_id(int(c))) for c in codes]
+
+
+def chain_overrides(arch: configs.LmArch, spec: ChainSpec) -> dict[str, tuple[np.ndarray, np.ndarray]]:
+    """{tensor name: (index, rows)} — rows (float32, bf16-exact) that replace tensor[index]
+    (rows of the embedding / gate / up; columns of down, given transposed)."""
+    if arch.hidden_size & (arch.hidden_size - 1) or spec.units + 1 > arch.hidden_size or \
+            spec.units > arch.intermediate_size or not arch.tie_word_embeddings:
+        raise ValueError("chain model needs a tied, power-of-two hidden size >= units + 1")
+    d = arch.hidden_size
+    vocab = configs.vocab_for(arch)
+    toks = chain_tokens(vocab, spec)
+    eos = vocab.speech_end_id
+    U = spec.units
+    H = hadamard_rows(list(range(1, U + 1)) + [spec.eos_row], d)  # chain rows, then EOS
+    s = np.float32(2.0 ** spec.emb_exp)
+    emb_idx = np.asarray(toks + [eos], dtype=np.int64)
+    emb_rows = H * s
+    gate = H[:U] * np.float32(2.0 ** spec.gate_exp)
+    down = np.zeros((U, d), dtype=np.float32)  # transposed: down[:, j] = down_t[j]
+    q = np.float32(2.0 ** spec.down_exp)
+    for j in range(U - 1):
+        if j % spec.eos_period == spec.eos_phase:
+            down[j] = q * (H[j + 1] + np.float32(2.0) * H[U])
+        elif j >= spec.lag:
+            down[j] = q * (H[j + 1] + np.float32(spec.w_seen) * H[j - spec.lag])
+        else:
+            down[j] = q * H[j + 1]
+    p = "model.layers.0."
+    unit_idx = np.arange(U, dtype=np.int64)
+    return {
+        "model.embed_tokens.weight": (emb_idx, emb_rows),
+        p + "mlp.gate_proj.weight": (unit_idx, gate),
+        p + "mlp.up_proj.weight": (unit_idx, gate),
+        p + "mlp.down_proj.weight.T": (unit_idx, down),
+    }
+
+
+def apply_chain(weights: dict[str, torch.Tensor], arch: configs.LmArch, spec: ChainSpec) -> None:
+    """Overwrites the chain rows in place (CPU or device tensors; bit-identical results)."""
+    for name, (idx, rows) in chain_overrides(arch, spec).items():
+        transposed = name.endswith(".T")
+        t = weights[name[:-2] if transposed else name]
+        ix = torch.from_numpy(idx).to(t.device)
+        v = torch.from_numpy(rows).to(device=t.device, dtype=t.dtype)
+        if transposed:
+            t[:, ix] = v.t()
+        else:
+            t[ix] = v
+
+
+def chain_prompt(vocab, spec: ChainSpec, utt: int, start: int, n_text_tokens: int, n_prompt_codes: int) -> list[int]:
+    """A synthetic prompt whose speech part ends with c_{start-lag-1} .. c_start, so that
+    decoding follows the chain from c_{start+1} and every lagged id is already seen."""
+    toks = chain_tokens(vocab, spec)
+    if start < spec.lag + 1 or start >= spec.units - 1:
+        raise ValueError("chain start out of range")
+    base = synthetic_prompt(vocab, utt, n_text_tokens, n_prompt_codes)
+    chain = set(toks)
+    base = [t for t in base if t not in chain]  # (random prompt codes never hit the chain)
+    return base + toks[start - spec.lag - 1: start + 1]
 
 
 # ---------------------------------------------------------------------- codec weights ---
