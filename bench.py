@@ -179,9 +179,17 @@ def main():
         fused = True
     except Exception:  # noqa: BLE001 (not this shape: separate launches)
         pass
-    # per-step share: the layer kernels once per layer, lm_head once
-    in_step = [k for k in kern if not (fused and k in ("qkv", "attention"))]
-    share = {k: kern[k]["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k in in_step}
+    # the one-row step as one persistent launch over all layers (lm_persist.hip)
+    persist = B == 1 and lm.decode_persistent()
+    if persist:
+        ms, by = lm.bench_kernel("persist", rows=1, ctx=ctx_mid, iters=max(3, args.kernel_iters // 3))
+        kern["persist"] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
+    # per-step share: the layer kernels once per layer (or the persistent launch once), lm_head once
+    if persist:
+        in_step = ["persist", "lm_head"]
+    else:
+        in_step = [k for k in kern if not (fused and k in ("qkv", "attention")) and k != "persist"]
+    share = {k: kern[k]["avg_ms"] * (1 if k in ("lm_head", "persist") else arch.num_layers) for k in in_step}
     dom = max(share, key=share.get)
     step_ms = lm_decode / max(dec_steps, 1)
     kv_ctx_bytes = B * arch.kv_bytes_per_token() * ctx_mid
@@ -196,10 +204,12 @@ def main():
         if hits:
             traffic = round(json.load(open(hits[-1]))["hbm_bytes_per_launch"])  # bytes per launch
             traffic_src = os.path.relpath(hits[-1], ROOT)
-    roofline = dict(bound="hbm", kernel=f"wgemm/{dom}" if dom != "attention" else "attn_decode",
+    kname = {"attention": "attn_decode", "persist": "persist_step (all layers, one launch)"}.get(dom, f"wgemm/{dom}")
+    roofline = dict(bound="hbm", kernel=kname,
                     achieved=round(kern[dom]["gbs"], 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(kern[dom]["gbs"] / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
                     bytes_per_launch=kern[dom]["bytes"], avg_launch_ms=round(kern[dom]["avg_ms"], 5),
+                    per_step_share_ms={k: round(v, 4) for k, v in share.items()},
                     decode_step=dict(ms=round(step_ms, 4), bytes=step_bytes,
                                      achieved_gbs=round(step_bytes / step_ms / 1e6, 1),
                                      frac=round(step_bytes / step_ms / 1e6 / HBM_PEAK_GBS, 4)),

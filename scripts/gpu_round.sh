@@ -22,6 +22,6 @@ for step in "$@"; do
     prof)
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o run -- \
         python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/${TAG}_prof.log 2>&1; rc=$?
-      tail -3 $OUT/${TAG}_prof.log; find $OUT/${TAG}_prof -name "*stats*"; stop_if_fatal $rc prof ;;
+      tail -3 $OUT/${TAG}_prof.log; find $OUT/${TAG}_prof -name "*trace*" -delete; find $OUT/${TAG}_prof -name "*stats*"; stop_if_fatal $rc prof ;;
   esac
 done

@@ -218,6 +218,13 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
   });
 }
 
+tts_status tts_lm_decode_path(tts_engine* e, int32_t* persistent) {
+  return guarded([&] {
+    TTS_REQUIRE(e && persistent, "null argument");
+    *persistent = lm_decode_persistent(reinterpret_cast<Engine*>(e)) ? 1 : 0;
+  });
+}
+
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes) {
   return guarded([&] {

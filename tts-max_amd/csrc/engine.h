@@ -84,6 +84,9 @@ struct LmWork {
   DevBuf x, xn, qkv, attn_out, act, q_rot, last_x;  // activations
   DevBuf part_o, part_ml;                           // attention split partials
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
+  DevBuf pgran, pflags, pseq;                       // persistent one-row step: granules, flags, tag
+  bool persist_ok = false;                          // the geometry runs the persistent step
+  int persist_ur[4] = {0, 0, 0, 0};
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
@@ -159,6 +162,7 @@ void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_l
               float* logits, hipStream_t s);
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes);
+bool lm_decode_persistent(Engine* e);
 
 // upload a named tensor to device memory as bf16 (convert from f32 if needed)
 void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging);

@@ -17,6 +17,7 @@
 #include <cstdio>
 
 #include "engine.h"
+#include "lm_persist.h"
 
 namespace tts {
 
@@ -131,6 +132,17 @@ void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::ve
     }
 }
 }  // namespace
+
+// the persistent step's hand-off state: granule tags 0xffffffff and flags 0 (never a step's
+// tag), step tag 1
+void persist_reset(Engine* e, hipStream_t s) {
+  LmWork& w = e->w;
+  HIP_CHECK(hipMemsetAsync(w.pgran.p, 0xff, w.pgran.bytes, s));
+  HIP_CHECK(hipMemsetAsync(w.pflags.p, 0, w.pflags.bytes, s));
+  const int one = 1;
+  HIP_CHECK(hipMemcpyAsync(w.pseq.p, &one, 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+}
 
 void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int n) {
   TTS_REQUIRE(cfgp != nullptr, "null config");
@@ -256,6 +268,15 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
+  w.persist_ok = persist_supported(HID, H, KVH, D, FF, L, S, w.nsplit_decode, w.split_decode, e->num_cu,
+                                   w.persist_ur);
+  if (w.persist_ok) {
+    w.pgran.alloc(persist_gran_elems(L) * 8);
+    w.pflags.alloc(persist_flag_elems(L) * 4);
+    w.pseq.alloc(64);
+    persist_init();
+    persist_reset(e, s);
+  }
   {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
     const int kmax = std::max(HID, std::max(FF, H * D));
     w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
@@ -291,6 +312,15 @@ bool use_split_attn() {
 // fattn_consumer): default on; TTS_FUSED_ATTN=0 keeps the separate attention launch.
 bool use_fused_attn() {
   static const bool v = !(getenv("TTS_FUSED_ATTN") && !atoi(getenv("TTS_FUSED_ATTN")));
+  return v;
+}
+
+// The one-row decode step as one persistent launch (lm_persist.hip) where the geometry
+// allows it: opt-in (TTS_PERSIST=1; bit-identical ids).  Measured 45 us per layer against
+// the per-layer launches' 40 (the hand-offs into streaming CUs cost ~2.5 us
+// each and the LDS rings hold only a third of a layer), so the launches stay the default.
+bool use_persist() {
+  static const bool v = getenv("TTS_PERSIST") && atoi(getenv("TTS_PERSIST"));
   return v;
 }
 
@@ -418,9 +448,45 @@ struct Ctx {
     return fx;
   }
 
+  unsigned long long* trace = nullptr;  // diagnostics (lm_bench_kernel, TTS_PERSIST_TRACE)
+
+  void persist_step(const int* slot, const int* pos) {
+    PersistArgs pa;
+    TTS_REQUIRE(c.num_layers <= PersistArgs::kMaxLayers, "persistent step: too many layers");
+    for (int l = 0; l < c.num_layers; ++l) {
+      const LmLayer& ly = M.layers[l];
+      pa.w[l][0] = ly.wqkv; pa.w[l][1] = ly.wo; pa.w[l][2] = ly.wgu; pa.w[l][3] = ly.wd;
+      pa.ln[l][0] = ly.ln1; pa.ln[l][1] = ly.ln2;
+    }
+    pa.L = c.num_layers;
+    pa.x = w.x.as<bf16_t>();
+    pa.row_slot = slot; pa.row_pos = pos;
+    pa.kv = w.kv.as<bf16_t>();
+    pa.kv_layer = (long long)c.max_batch * c.num_kv_heads * c.max_seq_len * c.head_dim;
+    pa.max_seq = c.max_seq_len;
+    pa.rope_cos = M.rope.as<bf16_t>();
+    pa.rope_sin = pa.rope_cos + (size_t)c.max_seq_len * c.head_dim;
+    pa.scale = (float)(1.0 / sqrt((double)c.head_dim));
+    pa.eps = c.rms_norm_eps;
+    pa.NS = w.nsplit_decode;
+    pa.gran = w.pgran.as<uint64_t>();
+    pa.flags = w.pflags.as<int>();
+    pa.err = w.ferr.as<int>();
+    pa.seq = w.pseq.as<int>();
+    pa.ur_qkv = w.persist_ur[0]; pa.ur_o = w.persist_ur[1]; pa.ur_gu = w.persist_ur[2]; pa.ur_d = w.persist_ur[3];
+    pa.trace = trace;
+    static const int warm = getenv("TTS_PERSIST_WARM") ? atoi(getenv("TTS_PERSIST_WARM")) : 1;
+    pa.warm = warm;
+    launch_persist_step(pa, s);
+  }
+
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
+    if (decode && rows == 1 && w.persist_ok && use_persist()) {
+      persist_step(slot, pos);
+      return;
+    }
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
     for (int l = 0; l < c.num_layers; ++l) {
@@ -724,8 +790,9 @@ int lm_gen_continue(Engine* e, int n_steps) {
   return G.finished ? 1 : 0;
 }
 
-// A fused QKV+attention launch whose granule wait timed out leaves garbage attention:
-// fail loudly at the next read (the flag is cleared for the next generation).
+// A fused QKV+attention launch (or persistent step) whose granule wait timed out leaves
+// garbage: fail loudly at the next read (the flag and the persistent step's hand-off state
+// are cleared for the next generation).
 static void check_fattn(Engine* e, hipStream_t s) {
   if (!e->w.ferr.p) return;
   int err = 0;
@@ -733,6 +800,7 @@ static void check_fattn(Engine* e, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
   if (err) {
     HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 4, s));
+    if (e->w.persist_ok) persist_reset(e, s);
     HIP_CHECK(hipStreamSynchronize(s));
     TTS_REQUIRE(false, "fused QKV+attention: a granule wait timed out (results invalid)");
   }
@@ -933,13 +1001,16 @@ void lm_slots_release(Engine* e, int slot) {
   Z.busy[slot] = 0;
 }
 
+bool lm_decode_persistent(Engine* e) { return e->lm.loaded && e->w.persist_ok && use_persist(); }
+
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 6 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
   TTS_REQUIRE(which != 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
+  TTS_REQUIRE(which != 7 || (rows == 1 && lm_decode_persistent(e)), "the persistent step needs one row (TTS-1 geometry)");
   hipStream_t s = e->stream;
   Ctx X(e, s);
   const tts_lm_config& c = X.c;
@@ -1022,6 +1093,13 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
             (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2;
         break;
       }
+      case 7:  // every layer of the one-row step as the persistent launch: all layers' weights,
+               // the K/V of ctx positions per layer, the new position's K/V, the row in / out
+        X.persist_step(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
+        b = (double)c.num_layers * (2.0 * (QKV * HID + HID * HD + 2.0 * FF * HID + HID * FF) + 4.0 * HID +
+                                    (double)c.num_kv_heads * (ctx + 1) * c.head_dim * 2 * 2) +
+            act_rw * 2 * HID;
+        break;
     }
   };
   launch();
@@ -1035,6 +1113,27 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   *avg_ms = ms / iters;
   *bytes = b;
   check_fattn(e, s);
+  // diagnostics: TTS_PERSIST_TRACE=<file> writes one traced persistent step's phase
+  // timestamps ([256][L][32] u64, 100 MHz clock) after the timed launches
+  const char* tf = getenv("TTS_PERSIST_TRACE");
+  if (which == 7 && tf && *tf) {
+    DevBuf tb;
+    const size_t n = (size_t)256 * c.num_layers * 32;
+    tb.alloc(n * 8);
+    HIP_CHECK(hipMemsetAsync(tb.p, 0, n * 8, s));
+    X.trace = tb.as<unsigned long long>();
+    X.persist_step(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
+    X.trace = nullptr;
+    std::vector<unsigned long long> h(n);
+    HIP_CHECK(hipMemcpyAsync(h.data(), tb.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    FILE* f = fopen(tf, "wb");
+    if (f) {
+      fwrite(h.data(), 8, n, f);
+      fclose(f);
+    }
+    check_fattn(e, s);
+  }
 }
 
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,

@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "tts_lm_score",
     "tts_lm_id_to_code",
     "tts_lm_last_timing",
+    "tts_lm_decode_path",
     "tts_lm_bench_kernel",
     "tts_codec_load",
     "tts_codec_decode",
@@ -167,6 +168,7 @@ def load_library() -> ctypes.CDLL:
         "tts_lm_score": (I32, [P, pi32, pi32, I32, I32, ctypes.POINTER(ctypes.c_float), P]),
         "tts_lm_id_to_code": (I32, [P, pi32, I32, pi32]),
         "tts_lm_last_timing": (I32, [P, ctypes.POINTER(F32), ctypes.POINTER(F32), pi32]),
+        "tts_lm_decode_path": (I32, [P, pi32]),
         "tts_lm_bench_kernel": (I32, [P, I32, I32, I32, I32, ctypes.POINTER(F32), ctypes.POINTER(ctypes.c_double)]),
         "tts_codec_load": (I32, [P, ctypes.POINTER(CodecConfig), ctypes.POINTER(TensorDesc), I32]),
         "tts_codec_decode": (I32, [P, pi32, pi32, I32, P, I32, ctypes.POINTER(ctypes.c_int64), P]),

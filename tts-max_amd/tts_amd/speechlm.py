@@ -317,6 +317,12 @@ class MI355XSpeechLM:
                                           out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), None))
         return torch.from_numpy(out)
 
+    def decode_persistent(self) -> bool:
+        """True when the one-row decode step runs as the persistent launch (lm_persist.hip)."""
+        v = ctypes.c_int32(0)
+        _lib.check(self._lib.tts_lm_decode_path(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
     def last_timing(self) -> tuple[float, float, int]:
         a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int32()
         _lib.check(self._lib.tts_lm_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
@@ -327,7 +333,9 @@ class MI355XSpeechLM:
     def bench_kernel(self, which: str, rows: int = 1, ctx: int = 450, iters: int = 50) -> tuple[float, float]:
         """(avg ms per launch, algorithmic bytes per launch) of one decode-step kernel."""
         ms, b = ctypes.c_float(), ctypes.c_double()
-        sel = 6 if which == "qkv_attn" else self.KERNELS.index(which)  # qkv_attn: QKV + fused attention
+        # qkv_attn: QKV + fused attention; persist: the whole one-row stack as one launch
+        sel = {"qkv_attn": 6, "persist": 7}.get(which)
+        sel = self.KERNELS.index(which) if sel is None else sel
         _lib.check(self._lib.tts_lm_bench_kernel(self._h, sel, rows, ctx, iters,
                                                  ctypes.byref(ms), ctypes.byref(b)))
         return ms.value, b.value
