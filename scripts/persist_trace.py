@@ -25,6 +25,7 @@ def main():
     ctx = int(sys.argv[1]) if len(sys.argv) > 1 else 452
     path = os.path.join(tempfile.gettempdir(), "persist_trace.bin")
     os.environ["TTS_PERSIST_TRACE"] = path
+    os.environ["TTS_PERSIST"] = "1"
     from tts_amd import configs
     from tts_amd.speechlm import MI355XSpeechLM
 

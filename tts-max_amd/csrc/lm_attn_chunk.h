@@ -48,45 +48,22 @@ TTS_DEV void attn_chunk_softmax(const bf16_t* Ks, const float* qg, int n, float 
 }
 
 // P.V for one head (lane = head dimension(s)): the chunk partial o of the lane's dimensions.
-// P.V over the chunk's positions: four fp32 accumulators per dimension (position tl goes
-// to accumulator tl % 4, each summed in position order), combined as (a0 + a1) + (a2 + a3):
-// four independent FMA chains instead of one (a single chain of 128 dependent FMA + select
-// pairs is latency-bound).  Positions at or beyond n contribute nothing (select).
 template <int D, int SPLIT>
 TTS_DEV void attn_chunk_pv(const bf16_t* Vs, const float* pg, int n, int lane, float (&o)[D / 64]) {
-  constexpr int KROW = D + 8, DPL = D / 64, PB = 16, NA = 4;
-  float acc[NA][DPL];
+  constexpr int KROW = D + 8, DPL = D / 64;
 #pragma unroll
-  for (int k = 0; k < NA; ++k)
-#pragma unroll
-    for (int e = 0; e < DPL; ++e) acc[k][e] = 0.f;
-  for (int t0 = 0; t0 < n; t0 += PB) {
-    float pb[PB];
-    uint32_t vb[PB];
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      const int tl = min(t0 + i, n - 1);  // (clamped: the extra terms are not added)
-      pb[i] = pg[tl];
-      if constexpr (DPL == 1) vb[i] = Vs[tl * KROW + lane];
-      else vb[i] = *(const uint32_t*)(Vs + tl * KROW + 2 * lane);
-    }
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-      const bool in = t0 + i < n;
-      float* a = acc[i % NA];
-      if constexpr (DPL == 1) {
-        const float nv = a[0] + pb[i] * bf2f((bf16_t)vb[i]);
-        a[0] = in ? nv : a[0];
-      } else {
-        const float n0 = a[0] + pb[i] * bf_lo(vb[i]);
-        const float n1 = a[1] + pb[i] * bf_hi(vb[i]);
-        a[0] = in ? n0 : a[0];
-        a[1] = in ? n1 : a[1];
-      }
+  for (int e = 0; e < DPL; ++e) o[e] = 0.f;
+#pragma unroll 8
+  for (int tl = 0; tl < n; ++tl) {
+    const float p = pg[tl];
+    if constexpr (DPL == 1) {
+      o[0] += p * bf2f(Vs[tl * KROW + lane]);
+    } else {
+      const uint32_t v2 = *(const uint32_t*)(Vs + tl * KROW + 2 * lane);
+      o[0] += p * bf_lo(v2);
+      o[1] += p * bf_hi(v2);
     }
   }
-#pragma unroll
-  for (int e = 0; e < DPL; ++e) o[e] = (acc[0][e] + acc[1][e]) + (acc[2][e] + acc[3][e]);
 }
 
 // ... and stores it with the chunk's (m, l)

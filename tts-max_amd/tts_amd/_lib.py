@@ -182,6 +182,8 @@ def load_library() -> ctypes.CDLL:
         "tts_op_gemm_f32": (I32, [P, I32, I32, I32, P, I32, P, P, I32, P, I32, P]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("TTS_LIB_PATH") and not hasattr(lib, name):
+            continue  # A/B runs against an older build (scripts/ab_bench.sh): its ABI subset
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -320,6 +320,8 @@ class MI355XSpeechLM:
     def decode_persistent(self) -> bool:
         """True when the one-row decode step runs as the persistent launch (lm_persist.hip)."""
         v = ctypes.c_int32(0)
+        if not hasattr(self._lib, "tts_lm_decode_path"):  # (an older build under A/B)
+            return False
         _lib.check(self._lib.tts_lm_decode_path(self._h, ctypes.byref(v)))
         return bool(v.value)
 
