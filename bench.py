@@ -13,9 +13,11 @@ batch 1 per GPU, P = 200 (150 prompt codes), N = 500 codes (10 s of audio), code
 (hop 160, ups [3]) on 650 codes.  Random-init weights of that architecture (no checkpoint
 is reachable offline); synthetic token ids of the reference prompt shape.
 
-Multi-GPU (torchrun): one process per GPU.  Rank 0 builds the request batch and
-broadcasts it over RCCL; each rank decodes its contiguous shard; generated codes are
-gathered back to rank 0 (the only exchange steps of the path).  Weak scaling.
+Multi-GPU (torchrun): one process per GPU (tts_amd/dp.py synthesize_sharded).  Rank 0
+builds the request batch and broadcasts it over RCCL; each rank generates and voices its
+contiguous shard (the reference's rank partition, quality_validation.py:171-182); codes
+and waveforms are gathered back to rank 0 (the only exchange steps of the path).  Weak
+scaling.
 
 Prints ONE JSON line (rank 0).
 """
@@ -56,13 +58,13 @@ def main():
     ap.add_argument("--text-tokens", type=int, default=39)
     ap.add_argument("--new", type=int, default=500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--cpu-steps", type=int, default=96)
     ap.add_argument("--kernel-iters", type=int, default=30)
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the N=1 secondary lines (bs=32 batched decode, bs=8 streaming latency)")
     args = ap.parse_args()
 
-    from tts_amd import configs, synth
+    from tts_amd import configs, dp, synth
     from tts_amd.codec import MI355XAudioDecoder
     from tts_amd.speechlm import MI355XSpeechLM
 
@@ -86,14 +88,9 @@ def main():
     B = args.batch
     N = args.new
 
-    # ---- requests: rank 0 builds all world*B prompts, broadcast over RCCL
+    # ---- requests: rank 0 builds all world*B prompts (broadcast over RCCL by dp.synthesize_sharded)
     prompts_all = [synth.synthetic_prompt(vocab, u, args.text_tokens, args.prompt_codes) for u in range(world * B)]
     P = max(len(p) for p in prompts_all)
-    req = torch.zeros(world * B, P + 1, dtype=torch.int32, device=dev)
-    if rank == 0:
-        for i, p in enumerate(prompts_all):
-            req[i, 0] = len(p)
-            req[i, 1:1 + len(p)] = torch.tensor(p, dtype=torch.int32)
 
     max_seq = P + N + 16
     t0 = time.time()
@@ -105,13 +102,16 @@ def main():
     codes_per_utt = args.prompt_codes + N
 
     def one_step(B=B, local_prompts=None):
-        if local_prompts is not None:
-            prompts = local_prompts
-        else:
-            if dist is not None:
-                dist.broadcast(req, src=0)
-            mine = req[rank * B:(rank + 1) * B].cpu()
-            prompts = [mine[i, 1:1 + int(mine[i, 0])].tolist() for i in range(B)]
+        if dist is not None and local_prompts is None:
+            # rank 0's request batch broadcast over RCCL, each rank generates +
+            # voices its contiguous shard, codes AND waveforms gathered to rank 0 (dp.py)
+            _, wavs, (n, _) = dp.synthesize_sharded(
+                prompts_all if rank == 0 else None, lm, dec, dev, max_new=N,
+                prompt_codes=lambda p: synthetic_codes(lm, p[-args.prompt_codes:]),
+                to_codes=lambda ids: synthetic_codes(lm, ids), balance="contiguous", min_new_tokens=N,
+                eos_token_id=vocab.speech_end_id, repetition_penalty=1.1, wav_out=wav_buf)
+            return n, wavs
+        prompts = local_prompts if local_prompts is not None else prompts_all[rank * B:(rank + 1) * B]
         new = lm.generate_batch(prompts, max_length=P + N, min_new_tokens=N, eos_token_id=vocab.speech_end_id,
                                 repetition_penalty=1.1)
         # codec input = prompt speech codes + generated codes.  Random-init weights emit
@@ -119,14 +119,6 @@ def main():
         # voiced as one code (synthetic_codes) so the codec workload has the configured size
         utts = [synthetic_codes(lm, p[-args.prompt_codes:] + n) for p, n in zip(prompts, new)]
         wav = dec.decode_batch(utts, out=wav_buf)
-        if local_prompts is not None:
-            return sum(len(n) for n in new), wav
-        out = torch.full((B, N), -1, dtype=torch.int32, device=dev)
-        for i, n in enumerate(new):
-            out[i, :len(n)] = torch.tensor(n, dtype=torch.int32)
-        if dist is not None:
-            gathered = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
-            dist.gather(out, gathered, dst=0)
         return sum(len(n) for n in new), wav
 
     wav_buf = torch.empty(max(B, 32 if secondary else 1) * codes_per_utt * carch.samples_per_code,
@@ -298,48 +290,72 @@ def synthetic_codes(lm, ids):
     return [c if c >= 0 else i % 65536 for i, c in zip(ids, lm.ids_to_codes(ids))]
 
 
+def _cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return model, os.cpu_count(), avail
+
+
 def cpu_baseline(arch, carch, prompt, N, args):
-    """The CPU oracle (a port of the reference path) on the host cores: a bounded sample
-    of the same workload (prefill of the same prompt + `cpu_steps` greedy steps, and the
-    codec on a proportional number of codes), scaled to codes/s for the full job."""
-    from oracle import codec_oracle, lm_oracle
-    from tts_amd import synth
+    """The reference's CPU path on the host cores, bounded sample of the same job: the
+    SpeechLM as transformers' own LlamaForCausalLM.generate (the arithmetic the reference
+    calls, tts/inference/inferencing.py:94-107: bf16, greedy, repetition penalty 1.1,
+    min_new_tokens) on the same synthetic weights — prefill of the same prompt + `cpu_steps`
+    generated codes — and the codec as the fp32 port (oracle/codec_oracle.py; the reference
+    codec cannot travel to the box) on a proportional number of codes; scaled to codes/s of
+    the full job."""
+    from oracle import codec_oracle
+    from oracle.hf_ref import hf_model
+    from tts_amd import configs, synth
 
     threads = torch.get_num_threads()
+    cpu_model, ncpu, avail = _cpu_info()
     t0 = time.time()
-    w = synth.lm_weights_cpu(arch, 0x5EED)
-    orc = lm_oracle.LlamaOracle(arch, {k: v.float() for k, v in w.items()}, max_seq_len=len(prompt) + N + 16,
-                                dtype=torch.float32)  # fp32 weights: no per-step conversion
-    del w
-    log(f"cpu baseline: weights ready in {time.time() - t0:.1f}s, {threads} threads")
+    model = hf_model(arch, synth.lm_weights_cpu(arch, 0x5EED))
+    log(f"cpu baseline: transformers model ready in {time.time() - t0:.1f}s, {threads} threads ({cpu_model})")
     S = args.cpu_steps
-    t1 = time.perf_counter()
-    cache = []
-    x = orc.forward(prompt, 0, cache)
-    t_prefill = time.perf_counter() - t1
-    seq = list(prompt)
-    t2 = time.perf_counter()
-    for i in range(S):
-        sc = orc.process(orc.logits(x[-1:])[0], seq, 1.1, i, N, -1)
-        tok = int(torch.argmax(sc))
-        seq.append(tok)
-        x = orc.forward([tok], len(seq) - 1, cache)
-    t_dec = (time.perf_counter() - t2) / S
+    ids = torch.tensor([prompt])
+    with torch.no_grad():
+        t1 = time.perf_counter()
+        model(ids)  # prefill alone (its time is subtracted from the generate call below)
+        t_prefill = time.perf_counter() - t1
+        t2 = time.perf_counter()
+        out = model.generate(input_ids=ids, max_length=len(prompt) + S, min_new_tokens=S,
+                             eos_token_id=configs.vocab_for(arch).speech_end_id, do_sample=False,
+                             repetition_penalty=1.1)
+        t_gen = time.perf_counter() - t2
+    assert out.shape[1] == len(prompt) + S
+    t_dec = max(t_gen - t_prefill, 1e-9) / (S - 1)  # the first new token comes from the prefill
+    del model
     cw = synth.codec_weights_cpu(carch, 0xC0DEC)
     T_s = 65
     t3 = time.perf_counter()
     codec_oracle.decode(cw, torch.randint(0, 65536, (T_s,)), carch.hop_length, carch.upsample_factors,
                         carch.kernel_sizes, carch.depth)
     t_codec_per_code = (time.perf_counter() - t3) / T_s
-    full = t_prefill + N * t_dec + (args.prompt_codes + N) * t_codec_per_code
+    full = t_prefill + (N - 1) * t_dec + (args.prompt_codes + N) * t_codec_per_code
     return {
         "value": round(N / full, 3),
         "unit": "audio-codes/s",
         "cores": threads,
-        "kind": "port",
-        "sample": (f"oracle (fp32 port of HF LlamaForCausalLM greedy + reference codec): prefill {len(prompt)} "
-                   f"tokens ({t_prefill:.2f}s) + {S} decode steps ({t_dec * 1000:.1f} ms/code) + codec on {T_s} "
-                   f"codes ({t_codec_per_code * 1000:.2f} ms/code), extrapolated to the {N}-code job"),
+        "kind": "reference",
+        "cpu": {"model": cpu_model, "nproc": ncpu, "affinity": avail, "torch_threads": threads},
+        "sample": (f"transformers {__import__('transformers').__version__} LlamaForCausalLM.generate (bf16, greedy, "
+                   f"rep 1.1; the reference's LM call) on the same weights: prefill {len(prompt)} tokens "
+                   f"({t_prefill:.2f}s) + {S} generated codes ({t_dec * 1000:.1f} ms/code), codec as the fp32 port "
+                   f"on {T_s} codes ({t_codec_per_code * 1000:.2f} ms/code); extrapolated to the {N}-code job "
+                   f"+ {args.prompt_codes + N}-code codec"),
     }
 
 

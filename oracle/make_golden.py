@@ -36,6 +36,7 @@ sys.path.insert(0, os.path.join(ROOT, "tts-max_amd"))
 sys.path.insert(0, ROOT)
 from tts_amd import configs, synth  # noqa: E402
 from oracle import codec_oracle, lm_oracle  # noqa: E402
+from oracle.hf_ref import hf_generate, hf_model  # noqa: E402
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
@@ -58,41 +59,6 @@ CODEC_CASES = {
     # the codec attention) and three lengths between
     "codec_24k_long": ("codec-24k", 0xC0DEC, [650, 300, 130, 65]),
 }
-
-
-def hf_model(arch, w):
-    """transformers LlamaForCausalLM (bf16, CPU) holding the synthetic weights `w`."""
-    from transformers import LlamaConfig, LlamaForCausalLM
-
-    cfg = LlamaConfig(**arch.hf_config_dict())
-    with torch.device("meta"):
-        model = LlamaForCausalLM(cfg)
-    model = model.to_empty(device="cpu").to(torch.bfloat16)
-    sd = dict(w)
-    if arch.tie_word_embeddings:
-        sd["lm_head.weight"] = w["model.embed_tokens.weight"]
-    missing, unexpected = model.load_state_dict(sd, strict=False)
-    missing = [m for m in missing if "rotary_emb" not in m]
-    assert not missing and not unexpected, (missing, unexpected)
-    model.model.rotary_emb = type(model.model.rotary_emb)(cfg)  # buffers were on meta
-    model.eval()
-    return model
-
-
-def hf_generate(model, prompt, max_length, min_new, eos, rep):
-    """The reference call (inferencing.py:94-107, greedy) -> (new ids, per-step top-2 margins
-    of the processed scores, per-step (top1, top2) ids)."""
-    with torch.no_grad():
-        out = model.generate(input_ids=torch.tensor([prompt]), max_length=max_length, min_new_tokens=min_new,
-                             eos_token_id=eos, do_sample=False, repetition_penalty=rep, top_p=1.0,
-                             temperature=0.0, output_scores=True, return_dict_in_generate=True)
-    new = out.sequences[0, len(prompt):].tolist()
-    margins, tops = [], []
-    for sc in out.scores:  # processed scores (penalty + min-new mask) of each step
-        top = torch.topk(sc[0].float(), 2)
-        margins.append(float(top.values[0] - top.values[1]))
-        tops.append([int(i) for i in top.indices])
-    return new, margins, tops
 
 
 def lm_fixture(name: str, manifest: dict) -> None:
@@ -305,6 +271,90 @@ def synth_fixture(name: str, manifest: dict) -> None:
     print(name, json.dumps(stats))
 
 
+# BASELINE configs[0] (tts_amd/config1.py): the 100 samples.jsonl utterances, RLHF pairing,
+# each through the reference's own _synthesize_audio (tiny LM, depth-2 codec).  Stored: the
+# generated ids (transformers' generate, recorded by a pass-through wrapper) and per-utterance
+# waveform statistics (length, sum of squares, 64 samples at fixed positions).
+CONFIG1_CASES = {"config1": ("tiny", 11, "codec-24k-d2", 0xC0DEC + 3)}
+
+
+class _Recorder:
+    """Passes model.generate through and keeps each call's output."""
+
+    def __init__(self, model):
+        self._m, self.calls = model, []
+
+    def generate(self, *a, **kw):
+        out = self._m.generate(*a, **kw)
+        self.calls.append(out)
+        return out
+
+    def __getattr__(self, k):
+        return getattr(self._m, k)
+
+
+def config1_fixture(name: str, manifest: dict) -> None:
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "shims"))
+    sys.path.insert(0, "/root/reference")
+    from tts.core.codec import decoding as ref_decoding
+    from tts.inference import inferencing as ref_inferencing
+
+    from tts_amd import config1
+
+    lm_arch_name, lm_seed, codec_name, codec_seed = CONFIG1_CASES[name]
+    arch = configs.LM_ARCHS[lm_arch_name]
+    carch = configs.CODEC_ARCHS[codec_name]
+    vocab = configs.vocab_for(arch)
+    t0 = time.time()
+    model = _Recorder(hf_model(arch, synth.lm_weights_cpu(arch, lm_seed)))
+    cw = synth.codec_weights_cpu(carch, codec_seed)
+    # the reference's AudioDecoder (its decode() and rate properties) around the reference
+    # Decoder reduced to the variant's depth (decoding.create always builds 12 blocks)
+    from tts.core.codec import decoder as ref_decoder
+
+    d = ref_decoder.Decoder(sample_rate=carch.sample_rate, hop_length=carch.hop_length,
+                            upsample_factors=list(carch.upsample_factors) or None,
+                            kernel_sizes=list(carch.kernel_sizes) or None)
+    d.decoder.backbone.transformers = torch.nn.Sequential(*list(d.decoder.backbone.transformers)[: carch.depth])
+    d.load_state_dict(cw, strict=True)
+    d.eval()
+    dec = ref_decoding.AudioDecoder.__new__(ref_decoding.AudioDecoder)
+    dec._device, dec._decoder = "cpu", d
+    dec._sample_rate, dec._token_rate = carch.sample_rate, carch.token_rate
+    samples = config1.load_samples("/root/reference/example/configs/samples.jsonl")
+    reqs = config1.requests(samples, vocab)
+    rec = dict(new_ids=[], new_lens=[], wav_lens=[], wav_ss=[], wav_pick=[])
+    for i, r in enumerate(reqs):
+        P = len(r["prompt_ids"])
+        st = ref_inferencing.InferenceSettings(temperature=0.0, max_tokens=P + r["n_new"], min_tokens=r["n_new"],
+                                               repetition_penalty=1.1)
+        wav, _ = ref_inferencing._synthesize_audio(model=model, tokenizer=_IdTokenizer(vocab, r["prompt_ids"]),
+                                                   audio_decoder=dec, speech_ids=r["speech_ids"], prompt="",
+                                                   model_device=torch.device("cpu"), inference_settings=st,
+                                                   use_vllm=False)
+        new = model.calls[-1][0, P:].tolist()
+        w = wav[0].double().numpy()
+        L = int(w.size)
+        pick = np.linspace(0, max(L - 1, 0), 64).astype(np.int64) if L else np.zeros(64, np.int64)
+        rec["new_ids"] += new
+        rec["new_lens"].append(len(new))
+        rec["wav_lens"].append(L)
+        rec["wav_ss"].append(float((w ** 2).sum()))
+        rec["wav_pick"].append(w[pick].astype(np.float32) if L else np.zeros(64, np.float32))
+        if i % 10 == 0:
+            print(name, i, P, len(new), L, flush=True)
+    rec["wav_pick"] = np.stack(rec["wav_pick"])
+    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), lm_arch=lm_arch_name, lm_seed=lm_seed,
+                        codec_arch=codec_name, codec_seed=codec_seed, **{k: np.asarray(v) for k, v in rec.items()})
+    manifest[name] = dict(kind="config1", lm_arch=lm_arch_name, codec_arch=codec_name, n=len(reqs),
+                          total_new=int(sum(rec["new_lens"])), total_samples=int(sum(rec["wav_lens"])),
+                          generator="reference tts.inference.inferencing._synthesize_audio per utterance "
+                          "(transformers generate; the reference AudioDecoder.decode around the reference Decoder at "
+                          "depth 2) on tts_amd.config1.requests (samples.jsonl, rlhf.py:56-67 pairing)",
+                          seconds=round(time.time() - t0, 1))
+    print(name, manifest[name])
+
+
 def codec_fixture(name: str, manifest: dict) -> None:
     sys.path.insert(0, os.path.join(ROOT, "oracle", "shims"))
     sys.path.insert(0, "/root/reference")
@@ -355,10 +405,11 @@ def main():
     mpath = os.path.join(GOLDEN, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     torch.manual_seed(0)
-    names = args.only or (list(LM_CASES) + list(CHAIN_CASES) + list(SYNTH_CASES) + list(CODEC_CASES))
+    names = args.only or (list(LM_CASES) + list(CHAIN_CASES) + list(SYNTH_CASES) + list(CONFIG1_CASES) +
+                          list(CODEC_CASES))
     for n in names:
         fn = (lm_fixture if n in LM_CASES else chain_fixture if n in CHAIN_CASES else
-              synth_fixture if n in SYNTH_CASES else codec_fixture)
+              synth_fixture if n in SYNTH_CASES else config1_fixture if n in CONFIG1_CASES else codec_fixture)
         fn(n, manifest)
         with open(mpath, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)

@@ -96,8 +96,12 @@ def _worker(rank, world, port, balance, q):
         return [[t * 2 + len(p) for t in p] + [len(p)] for p in batch]
 
     out = dp.run_sharded(prompts, 11, work, torch.device("cpu"), balance=balance)
+    # float payloads (waveforms) through the same ragged gather: item i = i * 0.5 + [0, 1, ...]
+    mine = dp.shard_of([[0] * (1 + i % 5) for i in range(11)], rank, world, balance)
+    fl = dp.gather_ragged({i: torch.arange(3 + 7 * (i % 4), dtype=torch.float32) + 0.5 * i for i in mine}, 11,
+                          torch.float32, torch.device("cpu"))
     if rank == 0:
-        q.put(out)
+        q.put((out, [f.tolist() for f in fl]))
     dist.destroy_process_group()
 
 
@@ -114,7 +118,8 @@ def test_dp_world2_gloo_equals_single(balance):
         p.join(timeout=60)
     prompts = [[i] * (1 + i % 5) for i in range(11)]
     ref = [[t * 2 + len(p) for t in p] + [len(p)] for p in prompts]
-    assert out == ref
+    assert out[0] == ref
+    assert out[1] == [(torch.arange(3 + 7 * (i % 4), dtype=torch.float32) + 0.5 * i).tolist() for i in range(11)]
 
 
 def test_codes_format_roundtrip_matches_reference_reader(tmp_path):

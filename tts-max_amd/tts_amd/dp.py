@@ -71,34 +71,58 @@ def broadcast_requests(prompts: Sequence[Sequence[int]] | None, device, src: int
     return out
 
 
-def gather_results(results: dict[int, list[int]], n_items: int, device, dst: int = 0) -> list[list[int]] | None:
-    """Each rank passes {item index: generated ids}; rank `dst` receives all items in order.
-    Variable lengths travel as one padded [n_items, Lmax+1] int32 block per rank (row i of a
-    rank's block is item i if that rank owns it, else length 0), reduced by a gather."""
+def gather_ragged(items: dict[int, Sequence], n_items: int, dtype: torch.dtype, device,
+                  dst: int = 0) -> list[torch.Tensor] | None:
+    """Each rank passes {item index: 1-D values} for the items it owns; rank `dst` returns
+    all n_items in index order (CPU tensors).  One flat payload per rank (its items
+    concatenated) and one int64 header [k, (index, length) * k], both padded to the longest
+    rank's (one all_reduce of two sizes) and moved by one gather each: the bytes on the
+    wire are the payload + 16 B per item, not n_items x the longest item per rank."""
     import torch.distributed as dist
 
-    world = dist.get_world_size()
-    Lmax = torch.tensor([max((len(v) for v in results.values()), default=0)], dtype=torch.int64, device=device)
-    dist.all_reduce(Lmax, op=dist.ReduceOp.MAX)
-    L = int(Lmax.item())
-    # row = [owned, len, ids...]
-    blk = torch.zeros(n_items, L + 2, dtype=torch.int32, device=device)
-    for i, ids in results.items():
-        blk[i, 0] = 1
-        blk[i, 1] = len(ids)
-        if ids:
-            blk[i, 2:2 + len(ids)] = torch.tensor(ids, dtype=torch.int32, device=device)
-    gl = [torch.empty_like(blk) for _ in range(world)] if dist.get_rank() == dst else None
-    dist.gather(blk, gl, dst=dst)
-    if dist.get_rank() != dst:
+    world, rank = dist.get_world_size(), dist.get_rank()
+    keys = sorted(items)
+    vals = [torch.as_tensor(items[i]).reshape(-1).to(dtype) for i in keys]
+    hdr = torch.tensor([len(keys)] + [x for i, v in zip(keys, vals) for x in (i, v.numel())], dtype=torch.int64)
+    pay = torch.cat(vals) if vals else torch.zeros(0, dtype=dtype)
+    sizes = torch.tensor([hdr.numel(), pay.numel()], dtype=torch.int64, device=device)
+    dist.all_reduce(sizes, op=dist.ReduceOp.MAX)
+    H, Pn = int(sizes[0]), int(sizes[1])
+    hb = torch.zeros(H, dtype=torch.int64, device=device)
+    hb[:hdr.numel()] = hdr.to(device)
+    pb = torch.zeros(max(Pn, 1), dtype=dtype, device=device)
+    pb[:pay.numel()] = pay.to(device)
+    hl = [torch.empty_like(hb) for _ in range(world)] if rank == dst else None
+    pl = [torch.empty_like(pb) for _ in range(world)] if rank == dst else None
+    dist.gather(hb, hl, dst=dst)
+    dist.gather(pb, pl, dst=dst)
+    if rank != dst:
         return None
-    out: list[list[int]] = [[] for _ in range(n_items)]
-    for g in gl:
-        g = g.cpu()
-        for i in range(n_items):
-            if int(g[i, 0]):
-                out[i] = g[i, 2:2 + int(g[i, 1])].tolist()
+    out: list[torch.Tensor | None] = [None] * n_items
+    for h, pv in zip(hl, pl):
+        h, pv = h.cpu().tolist(), pv.cpu()
+        off = 0
+        for j in range(h[0]):
+            i, L = h[1 + 2 * j], h[2 + 2 * j]
+            out[i] = pv[off:off + L].clone()
+            off += L
+    assert all(o is not None for o in out), "an item was not produced by any rank"
     return out
+
+
+def gather_results(results: dict[int, list[int]], n_items: int, device, dst: int = 0) -> list[list[int]] | None:
+    """Each rank passes {item index: generated ids}; rank `dst` receives all items in order."""
+    g = gather_ragged(results, n_items, torch.int32, device, dst)
+    return None if g is None else [t.tolist() for t in g]
+
+
+def shard_of(prompts: Sequence[Sequence[int]], rank: int, world: int, balance: str = "contiguous",
+             costs: Sequence[int] | None = None) -> list[int]:
+    """This rank's item indices: the reference's contiguous blocks, or LPT by cost (default:
+    prompt length)."""
+    if balance == "lpt":
+        return lpt_shard(list(costs) if costs is not None else [len(p) for p in prompts], rank, world)
+    return contiguous_shard(len(prompts), rank, world)
 
 
 def run_sharded(prompts: Sequence[Sequence[int]] | None, n_items: int, work: Callable[[list[list[int]]], list[list[int]]],
@@ -107,10 +131,39 @@ def run_sharded(prompts: Sequence[Sequence[int]] | None, n_items: int, work: Cal
     import torch.distributed as dist
 
     allp = broadcast_requests(prompts, device)
-    rank, world = dist.get_rank(), dist.get_world_size()
-    if balance == "lpt":
-        mine = lpt_shard([len(p) for p in allp], rank, world)
-    else:
-        mine = contiguous_shard(len(allp), rank, world)
+    mine = shard_of(allp, dist.get_rank(), dist.get_world_size(), balance)
     outs = work([allp[i] for i in mine]) if mine else []
     return gather_results({i: o for i, o in zip(mine, outs)}, len(allp), device)
+
+
+def synthesize_sharded(prompts: Sequence[Sequence[int]] | None, lm, decoder, device, *, max_new: int,
+                       prompt_codes: Callable[[list[int]], list[int]], to_codes: Callable[[list[int]], list[int]],
+                       balance: str = "contiguous", min_new_tokens: int = 0, eos_token_id: int = -1,
+                       repetition_penalty: float = 1.0, costs: Sequence[int] | None = None, wav_out=None):
+    """The whole DP job of BASELINE configs[3] / SURVEY §8e on this rank: broadcast the
+    request batch from rank 0, generate this rank's shard (greedy, `max_length` = longest
+    prompt + max_new), voice prompt codes + generated codes with the codec (one ragged
+    batch), gather codes AND waveforms to rank 0.  Returns (ids, wavs) on rank 0 (lists in
+    request order), (None, None) elsewhere, plus this rank's (n_codes, n_items)."""
+    import torch.distributed as dist
+
+    allp = broadcast_requests(prompts, device)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    mine = shard_of(allp, rank, world, balance, costs)
+    ids, wavs = {}, {}
+    if mine:
+        batch = [allp[i] for i in mine]
+        P = max(len(p) for p in allp)  # one max_length for every rank: per-row limits equal
+        new = lm.generate_batch(batch, max_length=P + max_new, min_new_tokens=min_new_tokens,
+                                eos_token_id=eos_token_id, repetition_penalty=repetition_penalty)
+        utts = [prompt_codes(p) + to_codes(n) for p, n in zip(batch, new)]
+        wl = decoder.decode_batch(utts, out=wav_out)  # host arrays, or views of wav_out in HBM
+        for i, n, w in zip(mine, new, wl):
+            ids[i] = n
+            wavs[i] = torch.as_tensor(w)
+    g_ids = gather_ragged(ids, len(allp), torch.int32, device)
+    g_wav = gather_ragged(wavs, len(allp), torch.float32, device)
+    n_codes = sum(len(v) for v in ids.values())
+    if g_ids is None:
+        return None, None, (n_codes, len(mine))
+    return [t.tolist() for t in g_ids], g_wav, (n_codes, len(mine))
