@@ -90,8 +90,6 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
     const float c = bf2f(qc[0]), sn = bf2f(qsn[0]);  // (tid < D: element 0 is dimension dk)
     const float rot = (dk < H2) ? -bf2f(kr) : bf2f(kr);
     const bf16_t kb = f2bf(rbf(rbf(bf2f(kx) * c) + rbf(rot * sn)));
-    a.kcache[cbase + (size_t)pos * D + dk] = kb;
-    a.vcache[cbase + (size_t)pos * D + dk] = vx;
     Ks[(pos - t0) * KROW + dk] = kb;
     Vs[(pos - t0) * KROW + dk] = vx;
   }
@@ -105,6 +103,12 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
     }
   }
   __syncthreads();
+  // the new position's k and v to the cache after the barrier (stores before it would be
+  // waited for inside it)
+  if (pos >= t0 && pos < t1 && tid < D) {
+    a.kcache[cbase + (size_t)pos * D + dk] = Ks[(pos - t0) * KROW + dk];
+    a.vcache[cbase + (size_t)pos * D + dk] = vx;
+  }
 
   // 4-6. scores (lane = position), chunk softmax statistics, P.V (lane = dimension)
   const int g = wave;

@@ -123,7 +123,7 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     raw[tid] = (uint32_t)v;
   }
   __syncthreads();
-  // RoPE of the group's q heads; the new position's roped k and v to the cache
+  // RoPE of the group's q heads and of the new position's k
   if (tid < G * D) {
     const int g = tid / D;
     qs[tid] = rope_elem(rawb[tid], rawb[g * D + (qd < H2 ? qd + H2 : qd - H2)], qd < H2, qc, qsn);
@@ -132,8 +132,6 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     const bf16_t kb = f2bf(rope_elem(rawb[G * D + tid], rawb[G * D + (tid < H2 ? tid + H2 : tid - H2)],
                                      tid < H2, qc, qsn));
     knew[tid] = kb;
-    a.kcache[cbase + (size_t)pos * D + tid] = kb;
-    a.vcache[cbase + (size_t)pos * D + tid] = rawb[G * D + D + tid];
   }
   for (int sp = c0; sp * SPLIT < ctx; sp += nslot) {
     const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx), n = t1 - t0;
@@ -154,6 +152,12 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
       attn_chunk_pv_store<D, SPLIT>(Vs, ps + wave * SPLIT, n, lane, m, l, a.part_o + pidx * D,
                                     a.part_ml + pidx * 2);
     }
+  }
+  // the new position's roped k and v to the cache, after the chunk math: a store issued
+  // before the loop would be waited for by its barriers (__syncthreads drains vmcnt)
+  if (has_new && tid < D) {
+    a.kcache[cbase + (size_t)pos * D + tid] = knew[tid];
+    a.vcache[cbase + (size_t)pos * D + tid] = rawb[G * D + D + tid];
   }
 }
 
