@@ -188,14 +188,18 @@ def main():
     step_bytes = arch.weight_bytes_per_step() + kv_ctx_bytes
     # HBM traffic of that kernel from the PMC passes of scripts/pmc_traffic.sh (FETCH_SIZE x2
     # + WRITE_SIZE per launch, committed under profiles/), when one exists for this shape
-    traffic, traffic_src = None, None
-    if arch.name == "tts1":
+    def pmc(k, rows):
+        """(HBM bytes per launch, source file) of kernel k at `rows` rows, or (None, None)."""
+        if arch.name != "tts1":
+            return None, None
         import glob
 
-        hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{dom}_{B}.json")))
-        if hits:
-            traffic = round(json.load(open(hits[-1]))["hbm_bytes_per_launch"])  # bytes per launch
-            traffic_src = os.path.relpath(hits[-1], ROOT)
+        hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{k}_{rows}.json")))
+        if not hits:
+            return None, None
+        return round(json.load(open(hits[-1]))["hbm_bytes_per_launch"]), os.path.relpath(hits[-1], ROOT)
+
+    traffic, traffic_src = pmc(dom, B)
     kname = {"attention": "attn_decode", "persist": "persist_step (all layers, one launch)"}.get(dom, f"wgemm/{dom}")
     roofline = dict(bound="hbm", kernel=kname,
                     achieved=round(kern[dom]["gbs"], 1), peak=HBM_PEAK_GBS, unit="GB/s",
@@ -205,7 +209,8 @@ def main():
                     decode_step=dict(ms=round(step_ms, 4), bytes=step_bytes,
                                      achieved_gbs=round(step_bytes / step_ms / 1e6, 1),
                                      frac=round(step_bytes / step_ms / 1e6 / HBM_PEAK_GBS, 4)),
-                    kernels={k: dict(avg_ms=round(v["avg_ms"], 5), gbs=round(v["gbs"], 1)) for k, v in kern.items()})
+                    kernels={k: dict(avg_ms=round(v["avg_ms"], 5), gbs=round(v["gbs"], 1), bytes=round(v["bytes"]),
+                                     traffic=pmc(k, B)[0]) for k, v in kern.items()})
 
     sec = None
     if secondary:
@@ -215,7 +220,7 @@ def main():
         one_step(32, p32)
         torch.cuda.synchronize()
         t = time.perf_counter()
-        reps = max(1, min(args.steps, 2))
+        reps = max(3, args.steps)
         n32 = sum(one_step(32, p32)[0] for _ in range(reps))
         torch.cuda.synchronize()
         e32 = (time.perf_counter() - t) / reps
@@ -223,6 +228,12 @@ def main():
         sec["bs32"] = dict(value=round(n32 / reps / e32, 2), unit="audio-codes/s", ms_per_step=round(1000 * e32, 3),
                            x_realtime=round(32 * N / carch.token_rate / e32, 2), lm_prefill_ms=round(a32, 3),
                            lm_decode_ms=round(b32, 3), decode_step_ms=round(b32 / max(k32, 1), 4))
+        # the 32-row decode kernels: live HIP-event time, algorithmic bytes, PMC HBM traffic
+        k32s = {}
+        for k in lm.KERNELS:
+            ms, by = lm.bench_kernel(k, rows=32, ctx=ctx_mid, iters=args.kernel_iters)
+            k32s[k] = dict(avg_ms=round(ms, 5), bytes=round(by), gbs=round(by / ms / 1e6, 1), traffic=pmc(k, 32)[0])
+        sec["bs32"]["kernels"] = k32s
         # configs[4]: streaming, bs=8, chunks of 25 codes voiced with 25 codes of left context
         from tts_amd.streaming import StreamingSynthesizer
 

@@ -1,5 +1,7 @@
 mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r2n_prof32 -o run -- python3 scripts/gen_probe.py 32 120 > gpurun_out/r2n_prof32.log 2>&1 || exit $?
-python scripts/step_breakdown.py $(find gpurun_out/r2n_prof32 -name "*kernel_trace.csv") > gpurun_out/r2n_break32.txt
-find gpurun_out/r2n_prof32 -name "*trace*" -delete
-cat gpurun_out/r2n_break32.txt
+for kr in "qkv_attn 1" "o_proj 1" "down 1" "lm_head 1" "qkv 32" "o_proj 32" "gate_up 32" "down 32" "attention 32" "lm_head 32"; do
+  set -- $kr
+  bash scripts/pmc_traffic.sh $1 $2 >> gpurun_out/pmc_all.log 2>&1 || exit $?
+  echo "done $1 $2" 
+done
+find gpurun_out/pmc -name "*.csv" -size +2M -delete
