@@ -214,7 +214,7 @@ typedef struct {
   int32_t depth;               /* 12 transformer blocks                               */
   int32_t heads;               /* 16                                                  */
   int32_t vq_dim;              /* 2048                                                */
-  int32_t max_codes;           /* largest T the workspaces are sized for              */
+  int32_t max_codes;           /* largest T of one utterance (tts_codec_decode rejects longer) */
 } tts_codec_config;
 
 tts_status tts_codec_load(tts_engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t,
@@ -223,7 +223,10 @@ tts_status tts_codec_load(tts_engine* e, const tts_codec_config* cfg, const tts_
 /* Decodes `batch` code sequences (host int32, concatenated, lengths in `lens`) into
  * waveforms.  wav: float32 [sum(lens) * samples_per_code] concatenated in input order;
  * wav_is_device != 0 means `wav` is a device pointer.  wav_lens (host) receives each
- * utterance's sample count. */
+ * utterance's sample count.  The batch runs as ragged passes of up to 32768 codes
+ * (TTS_CODEC_PASS_CODES): every GEMM over all utterances of a pass, GroupNorm / attention /
+ * overlap-add per utterance; an utterance's samples are bit-identical decoded alone or in
+ * any batch.  Returns after the waveforms are written (the stream is synchronised). */
 tts_status tts_codec_decode(tts_engine* e, const int32_t* codes, const int32_t* lens,
                             int32_t batch, float* wav, int32_t wav_is_device, int64_t* wav_lens,
                             void* stream);

@@ -16,7 +16,7 @@ for d in sys.argv[1:]:
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", "")
-            m = re.search(r"(gemm_bx3_kernel|gemm_f32_kernel|pgemm_kernel|wgemm_kernel)(<[^>(]*>)?", name)
+            m = re.search(r"(gemm_bx3_kernel|gemm_f32_kernel|pgemm_kernel|wgemm_kernel|codec_attn_kernel)(<[^>(]*>)?", name)
             if not m:
                 continue
             key = m.group(1) + (m.group(2) or "")

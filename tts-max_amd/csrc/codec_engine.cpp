@@ -4,10 +4,13 @@
 // Reference: tts/core/codec/decoder.py:69-89 (Decoder.forward), decoding.py:84-89
 // (AudioDecoder.decode), decoder_modules.py (Generator / VocosBackbone / ISTFTHead),
 // upsampler.py (UpSamplerBlock).  The reference decodes one utterance per call in fp32.
-// GroupNorm statistics and the unmasked attention span a whole utterance, so utterances
-// are never padded together: a batch is spread over kLanes streams,
-// each with its own workspace, and the utterances of different lanes run concurrently
-// (each one alone is far too small to fill 256 CUs).
+// A batch runs as ONE ragged pass: the utterances are stacked in each
+// time-major buffer with kCodecPad zero rows between them, every GEMM covers all of them
+// (M = sum T + gaps: one utterance alone is far too small to fill 256 CUs), and only the
+// ops that span an utterance take its bounds — GroupNorm statistics per utterance,
+// block-diagonal attention, ConvTranspose gather and overlap-add.  Every op computes a row
+// with the same arithmetic whatever the batch (the GEMM sums K in canonical chunks), so an
+// utterance's waveform is bit-identical decoded alone or in any batch.
 #include <math.h>
 #include <string.h>
 
@@ -19,7 +22,7 @@
 
 namespace tts {
 
-static constexpr int kPad = 3;  // zero rows before/after every time-major activation
+static constexpr int kPad = kCodecPad;  // zero rows before / after every utterance
 
 struct CodecResBlock {
   float *n1w, *n1b, *c1w, *c1b, *n2w, *n2b, *c2w, *c2b;  // conv weights re-laid [co][3*ci]
@@ -48,33 +51,14 @@ struct Codec {
   float* basis;                              // [nfft][ldh] windowed irfft basis
   float* window;                             // [nfft]
   int nfft = 0, nb = 0, ldh = 0;
-  int cap_T = 0, cap_F = 0;
-  // per-lane workspaces + streams
-  struct Lane {
-    DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
-    DevBuf gcodes, gwav;  // fixed input / output of the lane's captured graphs
-    DevBuf kpart;         // split-K GEMM partials
-    hipStream_t st = nullptr;
-    hipEvent_t done = nullptr;
-    std::map<int, hipGraphExec_t> graphs;  // one captured decode per utterance length
-    ~Lane() {
-      for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
-      if (done) (void)hipEventDestroy(done);
-      if (st) (void)hipStreamDestroy(st);
-    }
-  };
-  std::vector<std::unique_ptr<Lane>> lanes;
-  hipEvent_t start = nullptr;
+  int cap_T = 0;
+  // ragged-batch workspace, grown on demand (rows = padded rows of one pass)
+  DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
+  DevBuf meta;   // segment tables, wave offsets, code rows, attention query blocks
+  DevBuf planes;  // every GEMM weight (B operand) split once into its bf16 h / m / l planes
+  std::map<const float*, const uint16_t*> bplanes;
   DevBuf codes, wav;  // all utterances' codes; host-bound waveforms staged on the device
-  ~Codec() {
-    if (start) (void)hipEventDestroy(start);
-  }
 };
-
-static constexpr int kLanes = 4;  // = the HIP hardware queues per process (GPU_MAX_HW_QUEUES)
-static constexpr size_t kSplitElems = (size_t)4 << 20;  // split-K partial floats per lane
-// workspace of the lane whose launch sequence is being enqueued (decode_one)
-static thread_local float* t_split_ws = nullptr;
 
 void codec_destroy(Codec* c) { delete c; }
 
@@ -273,150 +257,226 @@ void codec_load(Engine* e, const tts_codec_config* cfgp, const tts_tensor_desc* 
                         p.second.size() * sizeof(float), hipMemcpyHostToDevice));
   for (auto& f : fixes) *f.dst = cd->weights.as<float>() + f.off;
 
-  // ---- workspaces
-  const int Tm = c.max_codes;
-  const int Fm = Tm * ups;
-  cd->cap_T = Tm;
-  cd->cap_F = Fm;
-  const size_t rows = (size_t)Fm + 2 * kPad;
-  size_t big = std::max((size_t)Tm * 4 * D, (size_t)Tm * VQ);
-  {  // ConvTranspose GEMM output Z = [Tc][k*Cout] at each stage's input length
-    int Tc = Tm;
-    for (auto& u : cd->ups) {
-      big = std::max(big, (size_t)Tc * u.k * u.Cout);
-      Tc *= u.u;
+  // ---- the GEMM weights' bf16x3 planes (the kernel would otherwise split every weight
+  // tile again in every workgroup of every launch)
+  {
+    std::vector<std::pair<const float*, size_t>> bw = {{cd->fc_w, (size_t)D * VQ}, {cd->emb_w, (size_t)D * 7 * D}};
+    auto rbw = [&](const CodecResBlock& rb) {
+      bw.push_back({rb.c1w, (size_t)rb.C * 3 * rb.C});
+      bw.push_back({rb.c2w, (size_t)rb.C * 3 * rb.C});
+    };
+    for (int i = 0; i < 2; ++i) { rbw(cd->prior[i]); rbw(cd->post[i]); }
+    for (auto& b : cd->tf) {
+      bw.push_back({b.c_attn, (size_t)3 * D * D});
+      bw.push_back({b.c_proj, (size_t)D * D});
+      bw.push_back({b.fc1, (size_t)4 * D * D});
+      bw.push_back({b.fc2, (size_t)4 * D * D});
     }
+    for (auto& u : cd->ups) {
+      bw.push_back({u.wz, (size_t)u.k * u.Cout * u.Cin});
+      rbw(u.rb);
+    }
+    if (cd->out_w) bw.push_back({cd->out_w, (size_t)D * C});
+    bw.push_back({cd->head_w, (size_t)cd->ldh * D});
+    bw.push_back({cd->basis, (size_t)nfft * cd->ldh});
+    size_t tot = 0;
+    for (auto& w : bw) tot += (3 * w.second + 127) & ~(size_t)127;
+    cd->planes.alloc(tot * 2);
+    size_t off = 0;
+    for (auto& w : bw) {
+      uint16_t* p = cd->planes.as<uint16_t>() + off;
+      launch_split_planes(w.first, p, (long long)w.second, nullptr);
+      cd->bplanes[w.first] = p;
+      off += (3 * w.second + 127) & ~(size_t)127;
+    }
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
   }
-  for (int l = 0; l < kLanes; ++l) {
-    auto ln = std::make_unique<Codec::Lane>();
-    ln->b0.alloc(rows * D * 4);
-    ln->b1.alloc(rows * D * 4);
-    ln->b2.alloc(rows * D * 4);
-    ln->big.alloc(big * 4);
-    ln->qkv.alloc((size_t)Tm * 3 * D * 4);
-    ln->stats.alloc(64 * 2 * 4);
-    ln->head.alloc((size_t)Fm * ldh * 4);
-    ln->spec.alloc((size_t)Fm * ldh * 4);
-    ln->frames.alloc((size_t)Fm * nfft * 4);
-    ln->gcodes.alloc((size_t)Tm * 4);
-    ln->kpart.alloc(kSplitElems * 4);
-    ln->gwav.alloc((size_t)Fm * c.hop_length * 4);
-    HIP_CHECK(hipStreamCreateWithFlags(&ln->st, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
-    cd->lanes.push_back(std::move(ln));
-  }
-  HIP_CHECK(hipEventCreateWithFlags(&cd->start, hipEventDisableTiming));
+
+  cd->cap_T = c.max_codes;
   if (e->codec) codec_destroy(e->codec);
   e->codec = cd.release();
 }
 
 namespace {
 
+thread_local const Codec* t_codec = nullptr;  // the codec whose pass is being enqueued
+
 void gemm(const float* A, int M, int K, int lda, const float* B, int N, const float* bias,
           float* C, int ldc, const float* resid, int act, hipStream_t s) {
   GemmF32Args g;
   g.A = A; g.M = M; g.K = K; g.lda = lda; g.B = B; g.N = N; g.bias = bias;
+  auto it = t_codec->bplanes.find(B);
+  if (it != t_codec->bplanes.end()) g.Bp = it->second;
   g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
-  g.part = t_split_ws; g.part_elems = t_split_ws ? kSplitElems : 0;
   launch_gemm_f32(g, s);
 }
 
-// ResnetBlock (decoder_modules.py:162-223) on a padded time-major buffer x (T rows of C at
-// row kPad); tmp is a padded scratch buffer; result written to out (padded, may alias none).
-void resnet(const CodecResBlock& rb, float* x, float* tmp, float* out, int T, float* stats,
-            hipStream_t s) {
+// The utterances of one pass at one time resolution: segment table (device), padded rows.
+struct Level {
+  const CodecSeg* seg = nullptr;
+  int rows = 0;   // padded rows of the buffer (kPad + sum (T + kPad))
+  int M = 0;      // GEMM rows: rows - 2 kPad (every utterance and the gaps between them)
+  int max_T = 0;
+};
+
+// ResnetBlock (decoder_modules.py:162-223) on ragged time-major buffers: x -> out, tmp is
+// scratch (its gap rows are the convs' zero padding, written by groupnorm_swish).
+void resnet(const CodecResBlock& rb, float* x, float* tmp, float* out, const Level& lv, int B,
+            float* stats, hipStream_t s) {
   const int C = rb.C;
   float* xr = x + (size_t)kPad * C;
   float* tr = tmp + (size_t)kPad * C;
   float* orow = out + (size_t)kPad * C;
-  launch_groupnorm_stats(xr, T, C, 32, 1e-6f, stats, s);
-  launch_groupnorm_swish(xr, T, C, 32, stats, rb.n1w, rb.n1b, tr, s);
+  launch_groupnorm_stats(x, lv.seg, B, C, 32, 1e-6f, stats, s);
+  launch_groupnorm_swish(x, lv.seg, B, lv.max_T, C, 32, stats, rb.n1w, rb.n1b, tmp, s);
   // conv1 (k=3, pad=1): sliding window starting one row above
-  gemm(tr - C, T, 3 * C, C, rb.c1w, C, rb.c1b, orow, C, nullptr, 0, s);
-  launch_groupnorm_stats(orow, T, C, 32, 1e-6f, stats, s);
-  launch_groupnorm_swish(orow, T, C, 32, stats, rb.n2w, rb.n2b, tr, s);
-  gemm(tr - C, T, 3 * C, C, rb.c2w, C, rb.c2b, orow, C, xr, 0, s);  // x + h
+  gemm(tr - C, lv.M, 3 * C, C, rb.c1w, C, rb.c1b, orow, C, nullptr, 0, s);
+  launch_groupnorm_stats(out, lv.seg, B, C, 32, 1e-6f, stats, s);
+  launch_groupnorm_swish(out, lv.seg, B, lv.max_T, C, 32, stats, rb.n2w, rb.n2b, tmp, s);
+  gemm(tr - C, lv.M, 3 * C, C, rb.c2w, C, rb.c2b, orow, C, xr, 0, s);  // x + h
+}
+
+void grow(DevBuf& b, size_t bytes) {
+  if (b.bytes < bytes) b.alloc(bytes);
 }
 
 }  // namespace
 
-// The whole Decoder.forward launch sequence of one utterance of T codes on lane `ln`
-// (stream `ls`): codes_in [T] int32 (device) -> wav_out [T * samples_per_code] f32 (device).
-static void decode_one(Codec& cd, Codec::Lane& ln, int T, const int* codes_in, float* wav_out,
-                       hipStream_t ls) {
+// Decoder.forward (decoder.py:69-89) of B utterances in one ragged pass: codes_dev = their
+// codes back to back (device), lens[b] codes each -> their waveforms back to back at wav_dev.
+static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, int B, float* wav_dev,
+                        hipStream_t s) {
   const tts_codec_config& c = cd.cfg;
   const int D = c.hidden_dim, H = c.heads, VQ = c.vq_dim;
-  int ups = 1;
-  for (int i = 0; i < c.n_upsample; ++i) ups *= c.upsample_factors[i];
-  t_split_ws = ln.kpart.as<float>();
-    const int F = T * ups;
-    const size_t rows_cap = (size_t)cd.cap_F + 2 * kPad;
-    // zero the padding rows (and everything else) of the three activation buffers
-    launch_zero(ln.b0.as<float>(), (long long)rows_cap * D, ls);
-    launch_zero(ln.b1.as<float>(), (long long)rows_cap * D, ls);
-    launch_zero(ln.b2.as<float>(), (long long)rows_cap * D, ls);
-    float* big = ln.big.as<float>();
-    float* b0 = ln.b0.as<float>();
-    float* b1 = ln.b1.as<float>();
-    float* b2 = ln.b2.as<float>();
-    float* stats = ln.stats.as<float>();
-    auto R = [&](float* buf, int C) { return buf + (size_t)kPad * C; };
-    // FSQ -> project_out -> fc_post_a
-    launch_fsq_project(codes_in, T, cd.po_w, cd.po_b, big, VQ, ls);
-    gemm(big, T, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, ls);
-    // embed Conv1d(k=7, pad=3): window starts 3 rows above
-    gemm(R(b0, D) - 3 * D, T, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, ls);
-    // prior_net: b1 -> b0 -> b1
-    resnet(cd.prior[0], b1, b2, b0, T, stats, ls);
-    resnet(cd.prior[1], b0, b2, b1, T, stats, ls);
-    // transformers on x = b1 (in place residual stream), scratch b2 / big / qkv
-    float* x = R(b1, D);
-    float* qkv = ln.qkv.as<float>();
-    for (int l = 0; l < c.depth; ++l) {
-      const CodecTfBlock& tb = cd.tf[l];
-      launch_rmsnorm_f32(x, T, D, tb.att_norm, 1e-6f, R(b2, D), ls);
-      gemm(R(b2, D), T, D, D, tb.c_attn, 3 * D, nullptr, qkv, 3 * D, nullptr, 0, ls);
-      launch_codec_rope(qkv, T, H, D / H, ls);
-      launch_codec_attention(qkv, T, H, D / H, R(b2, D), ls);
-      gemm(R(b2, D), T, D, D, tb.c_proj, D, nullptr, x, D, x, 0, ls);
-      launch_rmsnorm_f32(x, T, D, tb.ffn_norm, 1e-6f, R(b2, D), ls);
-      gemm(R(b2, D), T, D, D, tb.fc1, 4 * D, nullptr, big, 4 * D, nullptr, 1, ls);
-      gemm(big, T, 4 * D, 4 * D, tb.fc2, D, nullptr, x, D, x, 0, ls);
+  const int NU = (int)cd.ups.size();
+  // ---- segment tables of every time resolution, wave offsets, code rows, query blocks
+  std::vector<std::vector<CodecSeg>> seg(NU + 1, std::vector<CodecSeg>(B));
+  std::vector<Level> lv(NU + 1);
+  for (int i = 0; i <= NU; ++i) {
+    int row = kPad, mx = 0;
+    for (int b = 0; b < B; ++b) {
+      int T = lens[b];
+      for (int j = 0; j < i; ++j) T *= cd.ups[j].u;
+      seg[i][b] = {T, row};
+      row += T + kPad;
+      mx = std::max(mx, T);
     }
-    // post_net: b1 -> b0 -> b1
-    resnet(cd.post[0], b1, b2, b0, T, stats, ls);
-    resnet(cd.post[1], b0, b2, b1, T, stats, ls);
-    launch_layernorm_f32(R(b1, D), T, D, cd.ln_w, cd.ln_b, 1e-6f, R(b0, D), ls);
-    float* hid = R(b0, D);  // [T][D]
-    int Tc = T, C = D;
-    float* cur = b0;
-    for (size_t i = 0; i < cd.ups.size(); ++i) {
-      const CodecUp& u = cd.ups[i];
-      gemm(R(cur, C), Tc, u.Cin, u.Cin, u.wz, u.k * u.Cout, nullptr, big, u.k * u.Cout, nullptr, 0, ls);
-      float* nxt = (cur == b0) ? b1 : b0;
-      // clear stale rows of the destination so the padding below is zero again
-      launch_zero(nxt, (long long)rows_cap * D, ls);
-      launch_convt_gather(big, Tc, u.Cout, u.k, u.u, u.pad, u.bias, R(nxt, u.Cout), ls);
-      Tc *= u.u;
-      C = u.Cout;
-      launch_zero(b2, (long long)rows_cap * D, ls);
-      float* res_out = (nxt == b0) ? b1 : b0;
-      launch_zero(res_out, (long long)rows_cap * D, ls);
-      resnet(u.rb, nxt, b2, res_out, Tc, stats, ls);
-      cur = res_out;
-    }
-    if (!cd.ups.empty()) {
-      float* dst = (cur == b0) ? b1 : b0;
-      gemm(R(cur, C), Tc, C, C, cd.out_w, D, cd.out_b, R(dst, D), D, nullptr, 1, ls);
-      hid = R(dst, D);
-    }
-    // ISTFT head
-    gemm(hid, F, D, D, cd.head_w, cd.ldh, cd.head_b, ln.head.as<float>(), cd.ldh, nullptr, 0, ls);
-    launch_istft_spec(ln.head.as<float>(), F, cd.nb, cd.ldh, ln.spec.as<float>(), ls);
-    gemm(ln.spec.as<float>(), F, cd.ldh, cd.ldh, cd.basis, cd.nfft, nullptr, ln.frames.as<float>(),
-         cd.nfft, nullptr, 0, ls);
-    launch_ola(ln.frames.as<float>(), F, cd.nfft, c.hop_length, cd.window, wav_out, ls);
+    lv[i].rows = row;
+    lv[i].M = row - 2 * kPad;
+    lv[i].max_T = mx;
+  }
+  std::vector<long long> wav_off(B);
+  std::vector<int> code_row;
+  std::vector<int2> qblk;
+  long long w = 0;
+  for (int b = 0; b < B; ++b) {
+    wav_off[b] = w;
+    w += (long long)seg[NU][b].T * c.hop_length;
+    for (int t = 0; t < lens[b]; ++t) code_row.push_back(seg[0][b].row + t);
+    for (int q = 0; q < codec_attn_qblocks(lens[b]); ++q) qblk.push_back(make_int2(b, q * 64));
+  }
+  std::vector<char> host;
+  auto put = [&](const void* p, size_t n) {
+    const size_t off = host.size();
+    host.resize((off + n + 255) & ~(size_t)255);
+    memcpy(host.data() + off, p, n);
+    return off;
+  };
+  std::vector<size_t> seg_off(NU + 1);
+  for (int i = 0; i <= NU; ++i) seg_off[i] = put(seg[i].data(), sizeof(CodecSeg) * B);
+  const size_t wav_o = put(wav_off.data(), sizeof(long long) * B);
+  const size_t row_o = put(code_row.data(), sizeof(int) * code_row.size());
+  const size_t qb_o = put(qblk.data(), sizeof(int2) * qblk.size());
+  grow(cd.meta, host.size());
+  HIP_CHECK(hipMemcpyAsync(cd.meta.p, host.data(), host.size(), hipMemcpyHostToDevice, s));
+  char* mb = cd.meta.as<char>();
+  for (int i = 0; i <= NU; ++i) lv[i].seg = (const CodecSeg*)(mb + seg_off[i]);
+
+  // ---- workspace of this pass
+  int max_rows = 0;
+  for (auto& l : lv) max_rows = std::max(max_rows, l.rows);
+  const Level& L0 = lv[0];
+  const Level& LF = lv[NU];
+  size_t big = std::max((size_t)L0.rows * 4 * D, (size_t)L0.rows * VQ);
+  for (int i = 0; i < NU; ++i) big = std::max(big, (size_t)lv[i].rows * cd.ups[i].k * cd.ups[i].Cout);
+  grow(cd.b0, (size_t)max_rows * D * 4);
+  grow(cd.b1, (size_t)max_rows * D * 4);
+  grow(cd.b2, (size_t)max_rows * D * 4);
+  grow(cd.big, big * 4);
+  grow(cd.qkv, (size_t)L0.rows * 3 * D * 4);
+  grow(cd.stats, (size_t)B * 32 * 2 * 4);
+  grow(cd.head, (size_t)LF.rows * cd.ldh * 4);
+  grow(cd.spec, (size_t)LF.rows * cd.ldh * 4);
+  grow(cd.frames, (size_t)LF.rows * cd.nfft * 4);
+
+  t_codec = &cd;
+  float* b0 = cd.b0.as<float>();
+  float* b1 = cd.b1.as<float>();
+  float* b2 = cd.b2.as<float>();
+  float* bigp = cd.big.as<float>();
+  float* stats = cd.stats.as<float>();
+  auto R = [&](float* buf, int C) { return buf + (size_t)kPad * C; };
+  // FSQ -> project_out -> fc_post_a; the embed conv reads zero gaps
+  launch_fsq_project(codes_dev, (const int*)(mb + row_o), (int)code_row.size(), cd.po_w, cd.po_b, bigp, VQ, s);
+  gemm(R(bigp, VQ), L0.M, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, s);
+  launch_zero_gaps(b0, D, L0.seg, B, s);
+  // embed Conv1d(k=7, pad=3): window starts 3 rows above
+  gemm(R(b0, D) - 3 * D, L0.M, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, s);
+  // prior_net: b1 -> b0 -> b1
+  resnet(cd.prior[0], b1, b2, b0, L0, B, stats, s);
+  resnet(cd.prior[1], b0, b2, b1, L0, B, stats, s);
+  // transformers on x = b1 (in place residual stream), scratch b2 / big / qkv
+  float* x = R(b1, D);
+  float* qkv = cd.qkv.as<float>();
+  for (int l = 0; l < c.depth; ++l) {
+    const CodecTfBlock& tb = cd.tf[l];
+    launch_rmsnorm_f32(x, L0.M, D, tb.att_norm, 1e-6f, R(b2, D), s);
+    gemm(R(b2, D), L0.M, D, D, tb.c_attn, 3 * D, nullptr, R(qkv, 3 * D), 3 * D, nullptr, 0, s);
+    launch_codec_rope(R(qkv, 3 * D), L0.M, H, D / H, s);
+    launch_codec_attention(qkv, L0.seg, (const int2*)(mb + qb_o), (int)qblk.size(), H, D / H, b2, s);
+    gemm(R(b2, D), L0.M, D, D, tb.c_proj, D, nullptr, x, D, x, 0, s);
+    launch_rmsnorm_f32(x, L0.M, D, tb.ffn_norm, 1e-6f, R(b2, D), s);
+    gemm(R(b2, D), L0.M, D, D, tb.fc1, 4 * D, nullptr, R(bigp, 4 * D), 4 * D, nullptr, 1, s);
+    gemm(R(bigp, 4 * D), L0.M, 4 * D, 4 * D, tb.fc2, D, nullptr, x, D, x, 0, s);
+  }
+  // post_net: b1 -> b0 -> b1
+  resnet(cd.post[0], b1, b2, b0, L0, B, stats, s);
+  resnet(cd.post[1], b0, b2, b1, L0, B, stats, s);
+  launch_layernorm_f32(R(b1, D), L0.M, D, cd.ln_w, cd.ln_b, 1e-6f, R(b0, D), s);
+  float* hid = R(b0, D);
+  int C = D;
+  float* cur = b0;
+  for (int i = 0; i < NU; ++i) {
+    const CodecUp& u = cd.ups[i];
+    // ConvTranspose1d as Z = x . Wz^T (every tap of every input frame), then a gather
+    gemm(R(cur, C), lv[i].M, u.Cin, u.Cin, u.wz, u.k * u.Cout, nullptr, R(bigp, u.k * u.Cout), u.k * u.Cout,
+         nullptr, 0, s);
+    float* nxt = (cur == b0) ? b1 : b0;
+    launch_convt_gather(bigp, lv[i].seg, lv[i + 1].seg, B, lv[i + 1].max_T, u.Cout, u.k, u.u, u.pad, u.bias, nxt, s);
+    C = u.Cout;
+    float* res_out = (nxt == b0) ? b1 : b0;
+    resnet(u.rb, nxt, b2, res_out, lv[i + 1], B, stats, s);
+    cur = res_out;
+  }
+  if (NU > 0) {
+    float* dst = (cur == b0) ? b1 : b0;
+    gemm(R(cur, C), LF.M, C, C, cd.out_w, D, cd.out_b, R(dst, D), D, nullptr, 1, s);
+    hid = R(dst, D);
+  }
+  // ISTFT head
+  float* head = cd.head.as<float>();
+  float* spec = cd.spec.as<float>();
+  float* frames = cd.frames.as<float>();
+  gemm(hid, LF.M, D, D, cd.head_w, cd.ldh, cd.head_b, R(head, cd.ldh), cd.ldh, nullptr, 0, s);
+  launch_istft_spec(R(head, cd.ldh), LF.M, cd.nb, cd.ldh, R(spec, cd.ldh), s);
+  gemm(R(spec, cd.ldh), LF.M, cd.ldh, cd.ldh, cd.basis, cd.nfft, nullptr, R(frames, cd.nfft), cd.nfft, nullptr, 0,
+       s);
+  launch_ola(frames, LF.seg, (const long long*)(mb + wav_o), B, LF.max_T, cd.nfft, c.hop_length, cd.window, wav_dev,
+             s);
   HIP_CHECK(hipGetLastError());
+  // the host tables must outlive their upload
+  HIP_CHECK(hipStreamSynchronize(s));
 }
 
 void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, float* wav,
@@ -440,48 +500,22 @@ void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, f
   if (!wav_is_device && cd.wav.bytes < n_wav * 4) cd.wav.alloc(n_wav * 4);
   HIP_CHECK(hipMemcpyAsync(cd.codes.p, codes, n_codes * 4, hipMemcpyHostToDevice, s));
   float* wav_dev = wav_is_device ? wav : cd.wav.as<float>();
-  const int NL = std::min(B, kLanes);
-  HIP_CHECK(hipEventRecord(cd.start, s));
-  for (int l = 0; l < NL; ++l) HIP_CHECK(hipStreamWaitEvent(cd.lanes[l]->st, cd.start, 0));
-
-  // Each utterance replays its lane's graph for that length (captured on first use): ~150
-  // launches become one, which is what makes short streaming windows cheap.  The graph
-  // reads / writes the lane's fixed buffers; two device copies move codes and samples.
+  // passes of at most kPassCodes codes (the workspace grows with a pass: ~90 KB per code
+  // at 24 kHz); one utterance longer than that is a pass of its own
+  static const long long kPassCodes =
+      getenv("TTS_CODEC_PASS_CODES") ? atoll(getenv("TTS_CODEC_PASS_CODES")) : 32768;
   size_t off_codes = 0, off_wav = 0;
-  for (int b = 0; b < B; ++b) {
-    Codec::Lane& ln = *cd.lanes[b % NL];
-    const int T = lens[b];
-    const size_t L = (size_t)T * ups * c.hop_length;
-    auto it = ln.graphs.find(T);
-    if (it == ln.graphs.end()) {
-      if (ln.graphs.size() >= 32) {  // bounded cache: drop the smallest length
-        (void)hipGraphExecDestroy(ln.graphs.begin()->second);
-        ln.graphs.erase(ln.graphs.begin());
-      }
-      hipStream_t cs;
-      HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-      hipGraph_t g;
-      HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-      decode_one(cd, ln, T, ln.gcodes.as<int>(), ln.gwav.as<float>(), cs);
-      HIP_CHECK(hipStreamEndCapture(cs, &g));
-      hipGraphExec_t ge;
-      HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-      HIP_CHECK(hipGraphDestroy(g));
-      HIP_CHECK(hipStreamDestroy(cs));
-      it = ln.graphs.emplace(T, ge).first;
+  for (int b0 = 0; b0 < B;) {
+    int b1 = b0;
+    long long n = 0;
+    while (b1 < B && (b1 == b0 || n + lens[b1] <= kPassCodes)) n += lens[b1++];
+    decode_pass(cd, cd.codes.as<int>() + off_codes, lens + b0, b1 - b0, wav_dev + off_wav, s);
+    for (int b = b0; b < b1; ++b) {
+      wav_lens[b] = (int64_t)lens[b] * ups * c.hop_length;
+      off_wav += (size_t)wav_lens[b];
     }
-    HIP_CHECK(hipMemcpyAsync(ln.gcodes.p, cd.codes.as<int>() + off_codes, (size_t)T * 4,
-                             hipMemcpyDeviceToDevice, ln.st));
-    HIP_CHECK(hipGraphLaunch(it->second, ln.st));
-    HIP_CHECK(hipMemcpyAsync(wav_dev + off_wav, ln.gwav.p, L * 4, hipMemcpyDeviceToDevice, ln.st));
-    wav_lens[b] = (int64_t)L;
-    off_codes += T;
-    off_wav += L;
-  }
-  // join the lanes back into the caller's stream
-  for (int l = 0; l < NL; ++l) {
-    HIP_CHECK(hipEventRecord(cd.lanes[l]->done, cd.lanes[l]->st));
-    HIP_CHECK(hipStreamWaitEvent(s, cd.lanes[l]->done, 0));
+    off_codes += (size_t)n;
+    b0 = b1;
   }
   if (!wav_is_device) HIP_CHECK(hipMemcpyAsync(wav, wav_dev, n_wav * 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));

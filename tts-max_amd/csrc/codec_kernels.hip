@@ -197,7 +197,7 @@ static void launch_split(GemmF32Args g, int target, hipStream_t s) {
 // accumulation (v_mfma_f32_32x32x16_bf16, smallest terms first); the dropped terms are
 // <= 2^-24 relative, i.e. fp32 products.  Same tiles, staging order and epilogue as
 // gemm_f32_kernel.
-template <int TM, int TN>
+template <int TM, int TN, bool BPRE>
 __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
   constexpr int BK = 32, LS = BK + 8;           // bf16 row stride 80 B
   constexpr int MI = TM / 64, NJ = TN / 64;     // 32x32 accumulators per wave
@@ -217,6 +217,10 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
   const bool aok = ar < g.M, bok = br < g.N;
   const float* ap = g.A + (size_t)(aok ? ar : g.M - 1) * g.lda + kbeg + ak;
   const float* bp = g.B + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk;
+  // BPRE: B already split into its h / m / l planes (weights, split once at load)
+  const bf16_t* bq = BPRE ? (const bf16_t*)g.Bp + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk : nullptr;
+  const size_t bplane = (size_t)g.N * g.K;
+  const u32x4_t zq = {0u, 0u, 0u, 0u};
   f32x16_t acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -229,18 +233,30 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
   // two register sets: the global loads of step s+2 are in flight while step s computes
   // (unconditional, step index clamped: exact vmcnt waits)
   const int nsteps = (kend - kbeg) / BK;
-  float4 ra[2][KPA / 4], rb[2][KPB / 4];
-  auto load = [&](int st, float4 (&xa)[KPA / 4], float4 (&xb)[KPB / 4]) {
+  constexpr int RB = BPRE ? 1 : KPB / 4, RQ = BPRE ? KPB / 8 : 1;
+  float4 ra[2][KPA / 4], rb[2][RB];
+  u32x4_t rq[2][3][RQ];
+  auto load = [&](int st, float4 (&xa)[KPA / 4], float4 (&xb)[RB], u32x4_t (&xq)[3][RQ]) {
     const int kn = min(st, nsteps - 1) * BK;
 #pragma unroll
     for (int v = 0; v < KPA / 4; ++v) {
       const float4 l = *(const float4*)(ap + kn + 4 * v);
       xa[v] = aok ? l : z4;
     }
+    if constexpr (BPRE) {
 #pragma unroll
-    for (int v = 0; v < KPB / 4; ++v) {
-      const float4 l = *(const float4*)(bp + kn + 4 * v);
-      xb[v] = bok ? l : z4;
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int v = 0; v < RQ; ++v) {
+          const u32x4_t l = *(const u32x4_t*)(bq + pl * bplane + kn + 8 * v);
+          xq[pl][v] = bok ? l : zq;
+        }
+    } else {
+#pragma unroll
+      for (int v = 0; v < RB; ++v) {
+        const float4 l = *(const float4*)(bp + kn + 4 * v);
+        xb[v] = bok ? l : z4;
+      }
     }
   };
   // 8 fp32 -> 8 bf16 each of h, m, l (exact residuals: x - h and x - h - m are fp32-exact),
@@ -261,15 +277,24 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
     *(u32x4_t*)mp = m;
     *(u32x4_t*)lp = l;
   };
-  auto stage = [&](const float4 (&xa)[KPA / 4], const float4 (&xb)[KPB / 4]) {
+  auto stage = [&](const float4 (&xa)[KPA / 4], const float4 (&xb)[RB], const u32x4_t (&xq)[3][RQ]) {
 #pragma unroll
     for (int v = 0; v < KPA / 8; ++v)
       split8(xa[2 * v], xa[2 * v + 1], Ah + arow * LS + ak + 8 * v, Am + arow * LS + ak + 8 * v,
              Al + arow * LS + ak + 8 * v);
+    if constexpr (BPRE) {
 #pragma unroll
-    for (int v = 0; v < KPB / 8; ++v)
-      split8(xb[2 * v], xb[2 * v + 1], Bh + brow * LS + bk + 8 * v, Bm + brow * LS + bk + 8 * v,
-             Bl + brow * LS + bk + 8 * v);
+      for (int v = 0; v < RQ; ++v) {
+        *(u32x4_t*)(Bh + brow * LS + bk + 8 * v) = xq[0][v];
+        *(u32x4_t*)(Bm + brow * LS + bk + 8 * v) = xq[1][v];
+        *(u32x4_t*)(Bl + brow * LS + bk + 8 * v) = xq[2][v];
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < KPB / 8; ++v)
+        split8(xb[2 * v], xb[2 * v + 1], Bh + brow * LS + bk + 8 * v, Bm + brow * LS + bk + 8 * v,
+               Bl + brow * LS + bk + 8 * v);
+    }
   };
   auto compute = [&]() {
 #pragma unroll
@@ -304,18 +329,18 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
         }
     }
   };
-  load(0, ra[0], rb[0]);
-  load(1, ra[1], rb[1]);
+  load(0, ra[0], rb[0], rq[0]);
+  load(1, ra[1], rb[1], rq[1]);
   for (int st = 0; st < nsteps; st += 2) {
     __syncthreads();
-    stage(ra[0], rb[0]);
+    stage(ra[0], rb[0], rq[0]);
     __syncthreads();
-    load(st + 2, ra[0], rb[0]);
+    load(st + 2, ra[0], rb[0], rq[0]);
     compute();
     __syncthreads();
-    stage(ra[1], rb[1]);  // (an odd last step stages a clamped duplicate, not computed)
+    stage(ra[1], rb[1], rq[1]);  // (an odd last step stages a clamped duplicate, not computed)
     __syncthreads();
-    load(st + 3, ra[1], rb[1]);
+    load(st + 3, ra[1], rb[1], rq[1]);
     if (st + 1 < nsteps) compute();
   }
   // epilogue (as gemm_f32_kernel): lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -342,52 +367,55 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
   }
 }
 
-// split-K as launch_split, for the bf16x3 kernel (K chunks multiples of 32)
-template <int TM, int TN>
-static void launch_split_bx3(GemmF32Args g, int target, hipStream_t s) {
-  const int grid = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
-  int S = 1;
-  if (g.part != nullptr && grid < target * 3 / 4 && g.K >= 512) {
-    S = std::min(16, std::max(1, (target + grid - 1) / grid));
-    S = std::min(S, g.K / 256);
-    while (S > 1 && (size_t)S * g.M * g.N > g.part_elems) --S;
-  }
-  if (S <= 1) {
-    g.ksplit = 1; g.kchunk = g.K;
-    hipLaunchKernelGGL((gemm_bx3_kernel<TM, TN>), dim3(grid), dim3(256), 0, s, g);
-    return;
-  }
-  g.kchunk = ((g.K + S - 1) / S + 31) / 32 * 32;
-  S = (g.K + g.kchunk - 1) / g.kchunk;
-  g.ksplit = S;
-  hipLaunchKernelGGL((gemm_bx3_kernel<TM, TN>), dim3(grid, S), dim3(256), 0, s, g);
-  const long long n = (long long)g.M * g.N;
-  hipLaunchKernelGGL(gemm_f32_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g.part, S,
-                     g.M, g.N, g.bias, g.act, g.resid, g.C, g.ldc);
-}
-
-void launch_gemm_f32(const GemmF32Args& g, hipStream_t s) {
-  static const int target = getenv("TTS_CODEC_SPLIT_TARGET") ? atoi(getenv("TTS_CODEC_SPLIT_TARGET")) : 768;
+// The codec never splits K over workgroups: every output element is one in-order sweep of K
+// whatever the tile shape, so a row's bits do not depend on how many rows share the launch
+// (an utterance decodes to the same samples alone or in any batch).  A ragged batch gives
+// the GEMMs their rows; a lone short utterance leaves CUs idle instead.
+void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
+  GemmF32Args g = g_in;
+  g.part = nullptr;
+  g.ksplit = 1;
+  g.kchunk = g.K;
   // TTS_CODEC_BX3=0: plain fp32 MFMA for every contraction
   static const bool bx3 = !(getenv("TTS_CODEC_BX3") && !atoi(getenv("TTS_CODEC_BX3")));
   const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
   if (bx3 && g.K % 32 == 0 && g.lda % 4 == 0) {
-    if (big >= 256) launch_split_bx3<128, 128>(g, target, s);
-    else launch_split_bx3<64, 64>(g, target, s);
+    const dim3 g128(big), g64(((g.M + 63) / 64) * ((g.N + 63) / 64));
+    if (g.Bp && big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, true>), g128, dim3(256), 0, s, g);
+    else if (g.Bp) hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, true>), g64, dim3(256), 0, s, g);
+    else if (big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, false>), g128, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, false>), g64, dim3(256), 0, s, g);
     return;
   }
-  if (big >= 256) launch_split<128, 128>(g, target, s);
-  else launch_split<64, 64>(g, target, s);
+  if (big >= 256) launch_split<128, 128>(g, 0, s);
+  else launch_split<64, 64>(g, 0, s);
+}
+
+// B operand split once (weights at load): planes [3][n] = h, m, l with the kernel's rounding
+__global__ void split_planes_kernel(const float* __restrict__ x, bf16_t* __restrict__ p, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = x[i], h = rbf(v), r = v - h, m = rbf(r);
+    p[i] = f2bf(h);
+    p[n + i] = f2bf(m);
+    p[2 * n + i] = f2bf(r - m);
+  }
+}
+
+void launch_split_planes(const float* x, uint16_t* planes, long long n, hipStream_t s) {
+  const int grid = (int)std::min<long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(grid), dim3(256), 0, s, x, planes, n);
 }
 
 // ------------------------------------------------------------------ small kernels -----
 // ResidualFSQ(levels=[4]*8, num_quantizers=1).get_output_from_indices
 // (vector_quantize_pytorch 1.17.8): digit_j = (i // 4^j) % 4, code_j = (digit_j - 2) / 2,
 // scale 1 for quantizer 0, then project_out Linear(8 -> vq_dim).
-__global__ void fsq_project_kernel(const int* __restrict__ codes, const float* __restrict__ w,
-                                   const float* __restrict__ b, float* __restrict__ out, int vq) {
-  const int t = blockIdx.x;
-  const int c = codes[t];
+__global__ void fsq_project_kernel(const int* __restrict__ codes, const int* __restrict__ code_row,
+                                   const float* __restrict__ w, const float* __restrict__ b,
+                                   float* __restrict__ out, int vq) {
+  const int i = blockIdx.x;
+  const int c = codes[i];
+  const size_t t = (size_t)code_row[i];
   float z[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) z[j] = (float)(((c >> (2 * j)) & 3) - 2) * 0.5f;
@@ -399,16 +427,33 @@ __global__ void fsq_project_kernel(const int* __restrict__ codes, const float* _
   }
 }
 
-void launch_fsq_project(const int* codes, int T, const float* w, const float* b, float* out,
-                        int vq_dim, hipStream_t s) {
-  hipLaunchKernelGGL(fsq_project_kernel, dim3(T), dim3(256), 0, s, codes, w, b, out, vq_dim);
+void launch_fsq_project(const int* codes, const int* code_row, int n, const float* w, const float* b,
+                        float* out, int vq_dim, hipStream_t s) {
+  hipLaunchKernelGGL(fsq_project_kernel, dim3(n), dim3(256), 0, s, codes, code_row, w, b, out, vq_dim);
+}
+
+// The zero rows around the utterances of a ragged buffer (the padding a Conv1d window
+// reads): kPad rows before the first and after every utterance.
+__global__ void zero_gaps_kernel(float* __restrict__ x, int C, const CodecSeg* __restrict__ seg) {
+  const int g = blockIdx.x;
+  const size_t r0 = g == 0 ? 0 : (size_t)(seg[g - 1].row + seg[g - 1].T);
+  float* p = x + r0 * C;
+  for (int i = threadIdx.x; i < kCodecPad * C; i += blockDim.x) p[i] = 0.f;
+}
+
+void launch_zero_gaps(float* x, int C, const CodecSeg* seg, int B, hipStream_t s) {
+  hipLaunchKernelGGL(zero_gaps_kernel, dim3(B + 1), dim3(256), 0, s, x, C, seg);
 }
 
 // GroupNorm statistics (torch.nn.GroupNorm, biased variance), two passes in fp32.
-__global__ void groupnorm_stats_kernel(const float* __restrict__ x, int T, int C, int cg,
-                                       float eps, float* __restrict__ stats) {
+__global__ void groupnorm_stats_kernel(const float* __restrict__ x_all, const CodecSeg* __restrict__ seg,
+                                       int C, int cg, float eps, float* __restrict__ stats_all) {
   __shared__ float red[16];
   const int grp = blockIdx.x;
+  // one utterance per grid row: its own statistics over its own frames
+  const int T = seg[blockIdx.y].T;
+  const float* x = x_all + (size_t)seg[blockIdx.y].row * C;
+  float* stats = stats_all + (size_t)blockIdx.y * gridDim.x * 2;
   const long long n = (long long)T * cg;
   // thread -> (column c of the group, rows t0, t0 + rs, ...): no per-element integer
   // division, independent loads (the launcher guarantees blockDim % cg == 0)
@@ -431,31 +476,43 @@ __global__ void groupnorm_stats_kernel(const float* __restrict__ x, int T, int C
   }
 }
 
-void launch_groupnorm_stats(const float* x, int T, int C, int groups, float eps, float* stats,
-                            hipStream_t s) {
+void launch_groupnorm_stats(const float* x, const CodecSeg* seg, int B, int C, int groups, float eps,
+                            float* stats, hipStream_t s) {
   const int cg = C / groups;
   if (cg > 1024 || 1024 % cg != 0) throw std::runtime_error("groupnorm: channels per group must divide 1024");
-  hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(groups), dim3(1024), 0, s, x, T, C, cg, eps, stats);
+  hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(groups, B), dim3(1024), 0, s, x, seg, C, cg, eps, stats);
 }
 
-__global__ void groupnorm_swish_kernel(const float* __restrict__ x, int T, int C, int cg,
-                                       const float* __restrict__ stats,
+// y = swish(GN(x)) over each utterance's frames (grid row = utterance); the kPad rows
+// after each utterance (and before the first) are written as zeros: y is a Conv1d input
+__global__ void groupnorm_swish_kernel(const float* __restrict__ x_all, const CodecSeg* __restrict__ seg,
+                                       int C, int cg, int groups, const float* __restrict__ stats_all,
                                        const float* __restrict__ gamma,
-                                       const float* __restrict__ beta, float* __restrict__ y) {
-  const long long n = (long long)T * C;
+                                       const float* __restrict__ beta, float* __restrict__ y_all) {
+  const int b = blockIdx.y;
+  const size_t row = (size_t)seg[b].row;
+  const long long n = (long long)seg[b].T * C;
+  const float* x = x_all + row * C;
+  float* y = y_all + row * C;
+  const float* stats = stats_all + (size_t)b * groups * 2;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C), grp = c / cg;
     const float v = (x[i] - stats[2 * grp]) * stats[2 * grp + 1] * gamma[c] + beta[c];
     y[i] = v / (1.0f + expf(-v));
   }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)kCodecPad * C;
+       i += (long long)gridDim.x * blockDim.x) {
+    y[n + i] = 0.f;
+    if (b == 0) y_all[i] = 0.f;
+  }
 }
 
-void launch_groupnorm_swish(const float* x, int T, int C, int groups, const float* stats,
-                            const float* gamma, const float* beta, float* y, hipStream_t s) {
-  const long long n = (long long)T * C;
-  int grid = (int)std::min<long long>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(groupnorm_swish_kernel, dim3(grid), dim3(256), 0, s, x, T, C, C / groups,
+void launch_groupnorm_swish(const float* x, const CodecSeg* seg, int B, int max_T, int C, int groups,
+                            const float* stats, const float* gamma, const float* beta, float* y, hipStream_t s) {
+  const long long n = (long long)max_T * C;
+  int grid = (int)std::min<long long>((n + 255) / 256, std::max(1, 8192 / B));
+  hipLaunchKernelGGL(groupnorm_swish_kernel, dim3(grid, B), dim3(256), 0, s, x, seg, C, C / groups, groups,
                      stats, gamma, beta, y);
 }
 
@@ -521,132 +578,243 @@ void launch_codec_rope(float* qkv, int T, int heads, int hd, hipStream_t s) {
 }
 
 // ------------------------------------------------------------- codec attention --------
-// Non-causal SDPA (decoder_modules.py:283-285) for head_dim 64, fp32 flash attention on
-// v_mfma_f32_32x32x2_f32: one workgroup = one (head, 64-query block); keys in chunks of
-// 64 with online softmax.  Four waves own the 2x2 quadrants of every 64x64 tile.
-constexpr int AB = 64;   // query rows / key chunk
-constexpr int AD = 64;   // head dim
-constexpr int ALS = 65;  // padded LDS stride
+// Non-causal SDPA (decoder_modules.py:283-285) for head_dim 64 in fp32, as flash attention on
+// the bf16x3 MFMA form of the GEMM (every fp32 operand x = h + m + l, six bf16 products,
+// fp32 accumulation: fp32 products).  One workgroup = (utterance, 64-query block, head), four
+// waves of 16 queries each; keys in chunks of 64 with online softmax.  Per chunk the
+// workgroup stages K [key][d] and V^T [d][key] split into their three bf16 planes in LDS;
+// each wave computes its S = Q K^T (16 x 64) on v_mfma_f32_16x16x32_bf16, does the softmax
+// on the accumulators (a query row lives in one 16-lane DPP row), passes P through a private
+// LDS tile to re-read it as the A operand, and accumulates O += P V.
+constexpr int AB = 64;        // queries per workgroup / keys per chunk
+constexpr int AD = 64;        // head dim
+constexpr int APL = AB + 8;   // bf16 row stride of the K / V^T planes (144 B: conflict-free b128 reads)
+constexpr int APS = AB + 4;   // fp32 row stride of a wave's P tile
+constexpr size_t kAttnLds = 2 * 3 * 64 * APL * 2 + 4 * 16 * APS * 4;
 
-__global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict__ qkv, int T,
-                                                         int heads, float* __restrict__ out) {
-  extern __shared__ float sm[];
-  float* Qt = sm;                  // [AD][AB]   (k-major for A-operand reads)
-  float* Kt = Qt + AD * AB;        // [AD][AB]
-  float* Vs = Kt + AD * AB;        // [AB keys][AD]
-  float* Ss = Vs + AB * AD;        // [AB][ALS] scores
-  float* Pt = Ss + AB * ALS;       // [AB keys][AB rows]
-  float* mrow = Pt + AB * AB;      // [AB] running max
-  float* lrow = mrow + AB;         // [AB] running sum
-  float* arow = lrow + AB;         // [AB] rescale factor of this chunk
-  const int h = blockIdx.y, q0 = blockIdx.x * AB;
-  const int W = heads * AD, ld = 3 * W;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
-  const float scale = 0.125f;  // 1/sqrt(64)
-  // Q tile, transposed
-  for (int i = t; i < AB * AD / 4; i += 256) {
-    const int r = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q0 + r < T) v = *(const float4*)(qkv + (size_t)(q0 + r) * ld + h * AD + d4);
-    Qt[(d4 + 0) * AB + r] = v.x; Qt[(d4 + 1) * AB + r] = v.y;
-    Qt[(d4 + 2) * AB + r] = v.z; Qt[(d4 + 3) * AB + r] = v.w;
-  }
-  if (t < AB) { mrow[t] = -INFINITY; lrow[t] = 0.f; }
-  f32x16_t o;
+// 8 fp32 -> (h, m, l) bf16x8 planes with h + m + l == x (as split8 in gemm_bx3_kernel)
+TTS_DEV void split3(const float (&v)[8], u32x4_t& h, u32x4_t& m, u32x4_t& l) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
-
-  for (int k0 = 0; k0 < T; k0 += AB) {
-    __syncthreads();
-    for (int i = t; i < AB * AD / 4; i += 256) {
-      const int r = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
-      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-      if (k0 + r < T) {
-        kv = *(const float4*)(qkv + (size_t)(k0 + r) * ld + W + h * AD + d4);
-        vv = *(const float4*)(qkv + (size_t)(k0 + r) * ld + 2 * W + h * AD + d4);
-      }
-      Kt[(d4 + 0) * AB + r] = kv.x; Kt[(d4 + 1) * AB + r] = kv.y;
-      Kt[(d4 + 2) * AB + r] = kv.z; Kt[(d4 + 3) * AB + r] = kv.w;
-      *(float4*)(Vs + r * AD + d4) = vv;
-    }
-    __syncthreads();
-    // S quadrant = Q[wm] . K[wn]^T
-    f32x16_t sacc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
-#pragma unroll 8
-    for (int kk = 0; kk < AD / 2; ++kk) {
-      const int d = 2 * kk + (lane >> 5);
-      const float a = Qt[d * AB + wm * 32 + (lane & 31)];
-      const float b = Kt[d * AB + wn * 32 + (lane & 31)];
-      sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, sacc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int j = wn * 32 + (lane & 31);
-      Ss[i * ALS + j] = (k0 + j < T) ? sacc[r] * scale : -INFINITY;
-    }
-    __syncthreads();
-    // online softmax: 4 threads per row, 16 columns each
-    {
-      const int i = t >> 2, qd = t & 3;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) mx = fmaxf(mx, Ss[i * ALS + qd * 16 + j]);
-      mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-      const float mold = mrow[i];
-      const float mnew = fmaxf(mold, mx);
-      float ps = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float p = expf(Ss[i * ALS + qd * 16 + j] - mnew);
-        Pt[(qd * 16 + j) * AB + i] = p;
-        ps += p;
-      }
-      ps += __shfl_xor(ps, 1, 64);
-      ps += __shfl_xor(ps, 2, 64);
-      __syncthreads();  // everyone has read mrow[i] before it is updated
-      if (qd == 0) {
-        const float alpha = expf(mold - mnew);
-        arow[i] = alpha;
-        lrow[i] = lrow[i] * alpha + ps;
-        mrow[i] = mnew;
-      }
-    }
-    __syncthreads();
-    // O quadrant (rows wm, dims wn) = alpha * O + P . V
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] *= arow[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
-#pragma unroll 8
-    for (int kk = 0; kk < AB / 2; ++kk) {
-      const int k = 2 * kk + (lane >> 5);
-      const float a = Pt[k * AB + wm * 32 + (lane & 31)];
-      const float b = Vs[k * AD + wn * 32 + (lane & 31)];
-      o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, o, 0, 0, 0);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    const int d = wn * 32 + (lane & 31);
-    if (q0 + i < T) out[(size_t)(q0 + i) * W + h * AD + d] = o[r] / lrow[i];
+  for (int q = 0; q < 4; ++q) {
+    const float h0 = rbf(v[2 * q]), h1 = rbf(v[2 * q + 1]);
+    const float r0 = v[2 * q] - h0, r1 = v[2 * q + 1] - h1;
+    const float m0 = rbf(r0), m1 = rbf(r1);
+    h[q] = pack_bf2(h0, h1);
+    m[q] = pack_bf2(m0, m1);
+    l[q] = pack_bf2(r0 - m0, r1 - m1);
   }
 }
 
-void launch_codec_attention(const float* qkv, int T, int heads, int hd, float* out, hipStream_t s) {
-  const size_t lds = (size_t)(3 * AB * AD + AB * ALS + AB * AB + 3 * AB) * sizeof(float);
-  dim3 grid((T + AB - 1) / AB, heads);
-  hipLaunchKernelGGL(codec_attn_kernel, grid, dim3(256), lds, s, qkv, T, heads, out);
+// c += a . b over the three planes, smallest products first (as gemm_bx3_kernel)
+TTS_DEV f32x4_t mfma_x3(const u32x4_t (&a)[3], const u32x4_t (&b)[3], f32x4_t c) {
+  auto bf = [](const u32x4_t& x) { return __builtin_bit_cast(bf16x8_t, x); };
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[1]), bf(b[1]), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[2]), bf(b[0]), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[0]), bf(b[2]), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[1]), bf(b[0]), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[0]), bf(b[1]), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[0]), bf(b[0]), c, 0, 0, 0);
+}
+
+// max / sum over the 16 lanes of a DPP row (every lane ends with the same bits)
+TTS_DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x4E>(-INFINITY, v));
+  v = fmaxf(v, dpp_mov<0x141>(-INFINITY, v));
+  return fmaxf(v, dpp_mov<0x140>(-INFINITY, v));
+}
+TTS_DEV float row16_sum(float v) {
+  v += dpp_mov<0xB1>(0.f, v);
+  v += dpp_mov<0x4E>(0.f, v);
+  v += dpp_mov<0x141>(0.f, v);
+  return v + dpp_mov<0x140>(0.f, v);
+}
+
+__global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict__ qkv_all,
+                                                         const CodecSeg* __restrict__ seg,
+                                                         const int2* __restrict__ qblk, int heads,
+                                                         float* __restrict__ out_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Ks = (bf16_t*)smem;                 // [3][64 keys][APL]
+  bf16_t* Vt = Ks + 3 * 64 * APL;             // [3][64 d][APL]
+  float* Ps = (float*)(Vt + 3 * 64 * APL);    // [4 waves][16][APS]
+  // block-diagonal over a ragged batch: (utterance, query block, head), keys of that
+  // utterance only
+  const int2 qb = qblk[blockIdx.x];
+  const int h = blockIdx.y, q0 = qb.y;
+  const int T = seg[qb.x].T;
+  const int W = heads * AD, ld = 3 * W;
+  const float* qkv = qkv_all + (size_t)seg[qb.x].row * ld;
+  float* out = out_all + (size_t)seg[qb.x].row * W;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, c16 = lane & 15;
+  float* Pw = Ps + wave * 16 * APS;
+  const float scale = 0.125f;  // 1/sqrt(64), exact
+
+  // Q fragments (A operand, row = query c16 of the wave, d = 32 kk + 8 g + j), split once
+  u32x4_t qa[2][3];
+  {
+    const int q = q0 + wave * 16 + c16;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (q < T) {
+        const float4* p = (const float4*)(qkv + (size_t)q * ld + h * AD + kk * 32 + 8 * g);
+        const float4 a = p[0], b = p[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      split3(v, qa[kk][0], qa[kk][1], qa[kk][2]);
+    }
+  }
+  float mrow[4], lrow[4];
+  f32x4_t o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    mrow[r] = -INFINITY;
+    lrow[r] = 0.f;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // this thread's share of a chunk: K units (key, 8 d) u = t, t + 256; V^T unit (8 keys, 2 d)
+  const int dp = t & 31, kg = t >> 5;
+  float kreg[2][8], v0[8], v1[8];
+  auto load = [&](int k0) {  // global -> registers (zeros past the utterance's last key)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int u = t + 256 * it, key = u >> 3, d8 = (u & 7) * 8;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (k0 + key < T) {
+        const float4* p = (const float4*)(qkv + (size_t)(k0 + key) * ld + W + h * AD + d8);
+        a = p[0];
+        b = p[1];
+      }
+      kreg[it][0] = a.x; kreg[it][1] = a.y; kreg[it][2] = a.z; kreg[it][3] = a.w;
+      kreg[it][4] = b.x; kreg[it][5] = b.y; kreg[it][6] = b.z; kreg[it][7] = b.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float2 x = make_float2(0.f, 0.f);
+      if (k0 + 8 * kg + i < T) x = *(const float2*)(qkv + (size_t)(k0 + 8 * kg + i) * ld + 2 * W + h * AD + 2 * dp);
+      v0[i] = x.x;
+      v1[i] = x.y;
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < T; k0 += AB) {
+    __syncthreads();  // the previous chunk's K / V^T reads are done
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int u = t + 256 * it, key = u >> 3, d8 = (u & 7) * 8;
+      u32x4_t ph, pm, pl;
+      split3(kreg[it], ph, pm, pl);
+      *(u32x4_t*)(Ks + (0 * 64 + key) * APL + d8) = ph;
+      *(u32x4_t*)(Ks + (1 * 64 + key) * APL + d8) = pm;
+      *(u32x4_t*)(Ks + (2 * 64 + key) * APL + d8) = pl;
+    }
+    {
+      u32x4_t ph, pm, pl;
+      split3(v0, ph, pm, pl);
+      *(u32x4_t*)(Vt + (0 * 64 + 2 * dp) * APL + 8 * kg) = ph;
+      *(u32x4_t*)(Vt + (1 * 64 + 2 * dp) * APL + 8 * kg) = pm;
+      *(u32x4_t*)(Vt + (2 * 64 + 2 * dp) * APL + 8 * kg) = pl;
+      split3(v1, ph, pm, pl);
+      *(u32x4_t*)(Vt + (0 * 64 + 2 * dp + 1) * APL + 8 * kg) = ph;
+      *(u32x4_t*)(Vt + (1 * 64 + 2 * dp + 1) * APL + 8 * kg) = pm;
+      *(u32x4_t*)(Vt + (2 * 64 + 2 * dp + 1) * APL + 8 * kg) = pl;
+    }
+    __syncthreads();
+    if (k0 + AB < T) load(k0 + AB);  // next chunk in flight during this chunk's math
+    // S tile kt (keys 16 kt + c16 of lane's column; rows 4 g + r)
+    f32x4_t sc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      sc[kt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4_t kb[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          kb[pl] = *(const u32x4_t*)(Ks + (pl * 64 + 16 * kt + c16) * APL + kk * 32 + 8 * g);
+        sc[kt] = mfma_x3(qa[kk], kb, sc[kt]);
+      }
+    }
+    // online softmax per query row (rows 4 g + r: one DPP row of 16 lanes)
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const float sv = (k0 + 16 * kt + c16 < T) ? sc[kt][r] * scale : -INFINITY;
+        sc[kt][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+      mx = row16_max(mx);
+      const float mnew = fmaxf(mrow[r], mx);
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const float p = expf(sc[kt][r] - mnew);
+        Pw[(4 * g + r) * APS + 16 * kt + c16] = p;
+        ps += p;
+      }
+      ps = row16_sum(ps);
+      alpha[r] = expf(mrow[r] - mnew);
+      lrow[r] = lrow[r] * alpha[r] + ps;
+      mrow[r] = mnew;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha[r];
+    // O += P V: A = P (row = query c16, keys 32 kk + 8 g + j) from the wave's own tile
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4_t pa[3];
+      {
+        const float4* p = (const float4*)(Pw + c16 * APS + kk * 32 + 8 * g);
+        const float4 a = p[0], b = p[1];
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        split3(v, pa[0], pa[1], pa[2]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        u32x4_t vb[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          vb[pl] = *(const u32x4_t*)(Vt + (pl * 64 + 16 * dt + c16) * APL + kk * 32 + 8 * g);
+        o[dt] = mfma_x3(pa, vb, o[dt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + wave * 16 + 4 * g + r;
+    if (q >= T) continue;
+    const float inv = 1.0f / lrow[r];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) out[(size_t)q * W + h * AD + 16 * dt + c16] = o[dt][r] * inv;
+  }
+}
+
+int codec_attn_qblocks(int T) { return (T + AB - 1) / AB; }
+
+void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
+                            int hd, float* out, hipStream_t s) {
+  if (hd != AD) throw std::runtime_error("codec attention: head_dim 64 expected");
+  dim3 grid(nqblk, heads);
+  hipLaunchKernelGGL(codec_attn_kernel, grid, dim3(256), kAttnLds, s, qkv, seg, qblk, heads, out);
 }
 
 // ConvTranspose1d(stride u, padding pad) from Z[t][j*Cout + co] = sum_ci x[t][ci] W[ci][co][j]:
 // output t' receives tap j from input t with t*u - pad + j = t'.
-__global__ void convt_gather_kernel(const float* __restrict__ Z, int T, int Cout, int k, int u,
-                                    int pad, const float* __restrict__ bias, float* __restrict__ y) {
-  const int To = T * u;
+__global__ void convt_gather_kernel(const float* __restrict__ Z_all, const CodecSeg* __restrict__ seg_in,
+                                    const CodecSeg* __restrict__ seg_out, int Cout, int k, int u, int pad,
+                                    const float* __restrict__ bias, float* __restrict__ y_all) {
+  const int b = blockIdx.y;
+  const int T = seg_in[b].T, To = seg_out[b].T;
+  const float* Z = Z_all + (size_t)seg_in[b].row * k * Cout;
+  float* y = y_all + (size_t)seg_out[b].row * Cout;
   const long long n = (long long)To * Cout;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -663,11 +831,11 @@ __global__ void convt_gather_kernel(const float* __restrict__ Z, int T, int Cout
   }
 }
 
-void launch_convt_gather(const float* Z, int T, int Cout, int k, int u, int pad,
-                         const float* bias, float* y, hipStream_t s) {
-  const long long n = (long long)T * u * Cout;
-  int grid = (int)std::min<long long>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(convt_gather_kernel, dim3(grid), dim3(256), 0, s, Z, T, Cout, k, u, pad,
+void launch_convt_gather(const float* Z, const CodecSeg* seg_in, const CodecSeg* seg_out, int B, int max_To, int Cout,
+                         int k, int u, int pad, const float* bias, float* y, hipStream_t s) {
+  const long long n = (long long)max_To * Cout;
+  int grid = (int)std::min<long long>((n + 255) / 256, std::max(1, 8192 / B));
+  hipLaunchKernelGGL(convt_gather_kernel, dim3(grid, B), dim3(256), 0, s, Z, seg_in, seg_out, Cout, k, u, pad,
                      bias, y);
 }
 
@@ -696,8 +864,13 @@ void launch_istft_spec(const float* head, int F, int nb, int ld, float* spec, hi
 
 // ISTFT 'same' overlap-add (decoder_modules.py:64-93): frames are already irfft'ed and
 // windowed; y[i] = sum_f frames[f][i+pad-f*hop] / sum_f window^2[i+pad-f*hop].
-__global__ void ola_kernel(const float* __restrict__ frames, int F, int nfft, int hop,
-                           const float* __restrict__ win, float* __restrict__ y) {
+__global__ void ola_kernel(const float* __restrict__ frames_all, const CodecSeg* __restrict__ seg,
+                           const long long* __restrict__ wav_off, int nfft, int hop,
+                           const float* __restrict__ win, float* __restrict__ y_all) {
+  const int b = blockIdx.y;
+  const int F = seg[b].T;
+  const float* frames = frames_all + (size_t)seg[b].row * nfft;
+  float* y = y_all + wav_off[b];
   const int pad = (nfft - hop) / 2;
   const long long L = (long long)F * hop;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < L;
@@ -719,11 +892,11 @@ __global__ void ola_kernel(const float* __restrict__ frames, int F, int nfft, in
   }
 }
 
-void launch_ola(const float* frames, int F, int nfft, int hop, const float* window, float* y,
-                hipStream_t s) {
-  const long long L = (long long)F * hop;
-  int grid = (int)std::min<long long>((L + 255) / 256, 8192);
-  hipLaunchKernelGGL(ola_kernel, dim3(grid), dim3(256), 0, s, frames, F, nfft, hop, window, y);
+void launch_ola(const float* frames, const CodecSeg* seg, const long long* wav_off, int B, int max_F, int nfft,
+                int hop, const float* window, float* y, hipStream_t s) {
+  const long long L = (long long)max_F * hop;
+  int grid = (int)std::min<long long>((L + 255) / 256, std::max(1, 8192 / B));
+  hipLaunchKernelGGL(ola_kernel, dim3(grid, B), dim3(256), 0, s, frames, seg, wav_off, nfft, hop, window, y);
 }
 
 __global__ void zero_kernel(float* p, long long n) {
