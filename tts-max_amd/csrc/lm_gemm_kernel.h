@@ -812,6 +812,17 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
     if (!EARLY) throw std::runtime_error("wgemm: fused attention needs the register-staged prologue");
     lds = std::max(lds, fattn_lds_bytes());
     grid += a.fattn_wgs;
+    // The appended consumers spin on the projection workgroups' granules: every workgroup of
+    // the grid must be resident at once (the consumers, dispatched last, could otherwise hold
+    // CUs a producer waits for).  One workgroup per CU always fits, so grid <= CUs suffices.
+    static const int cus = [] {
+      int n = 0;
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n;
+    }();
+    if (grid > cus) throw std::runtime_error("wgemm: fused attention grid exceeds one workgroup per CU");
   }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
   const dim3 g(grid, a.sliced ? a.kc : 1);
