@@ -6,9 +6,10 @@ launches (TTS_PERSIST=0): the same arithmetic, so the same greedy ids, id for id
 Random TTS-1 weights (non-decisive: bf16 near-ties are frequent at V = 193,856, so any
 difference in a single rounding would flip ids within a few hundred steps), prompts of the
 reference's shape, contexts crossing every 128-position attention chunk of max_seq_len 1024
-(8 chunks: the merge's chunk groups of two) and 512 (4 chunks: groups of one).  The decisive
-transformers fixture runs through the persistent step in tests/test_gpu_chain.py (it is the
-default one-row path)."""
+(8 chunks: the merge's chunk groups of two) and 512 (4 chunks: groups of one).  The
+persistent step is opt-in (TTS_PERSIST=1; DESIGN.md §3.5: slower than the launches), so the
+decisive transformers fixture (tests/test_gpu_chain.py) runs through the launches, and
+this equality carries it over to the persistent step."""
 
 import json
 import os

@@ -475,8 +475,6 @@ struct Ctx {
     pa.seq = w.pseq.as<int>();
     pa.ur_qkv = w.persist_ur[0]; pa.ur_o = w.persist_ur[1]; pa.ur_gu = w.persist_ur[2]; pa.ur_d = w.persist_ur[3];
     pa.trace = trace;
-    static const int warm = getenv("TTS_PERSIST_WARM") ? atoi(getenv("TTS_PERSIST_WARM")) : 1;
-    pa.warm = warm;
     launch_persist_step(pa, s);
   }
 

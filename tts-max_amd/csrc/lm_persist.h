@@ -28,7 +28,6 @@ struct PersistArgs {
   int* err = nullptr;                   // set when a wait timed out
   int* seq = nullptr;                   // the step's tag (>= 1), advanced by the launch
   int ur_qkv = 0, ur_o = 0, ur_gu = 0, ur_d = 0;  // units per round of each matrix's layout
-  int warm = 1;                         // role A warms the Infinity Cache with the next phases' tiles
   unsigned long long* trace = nullptr;  // diagnostics: [256][L][32] phase timestamps (100 MHz) or null
 };
 
