@@ -29,7 +29,7 @@ print(json.dumps(r))
 var, rows = sys.argv[1], sys.argv[2]
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 for rd in range(rounds):
-    for v in ("0", "1"):
+    for v in (os.environ.get("AB_V0", "0"), os.environ.get("AB_V1", "1")):
         env = dict(os.environ, **{var: v})
         out = subprocess.run([sys.executable, "-c", CHILD, ROOT, rows], env=env, capture_output=True, text=True,
                              timeout=300)

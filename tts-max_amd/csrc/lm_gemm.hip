@@ -148,6 +148,13 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
       wgemm_lds_bytes(w, ks, ng, M, K / p.sp.kc, true) <= kLdsBudget) {
     p.a_lds = true;
     p.sliced = true;
+    // one round of workgroups over all K chunks: each stages its A chunk (up to 128 KiB)
+    // once and walks several units grid-stride (tiles are addressed by the layout's rounds,
+    // so the launch grid is free).  TTS-1 down at 32 rows: 128 x 4 workgroups in two rounds,
+    // each staging 128 KiB of A for 64 KiB of weights -> 64 x 4: 19.5 -> 15.6 us, step
+    // 1,228 -> 1,179 us, same ids (profiles/r2_ab_sliced_grid.txt).  TTS_SLICED_GRID=0: off.
+    static const bool one_round = !(getenv("TTS_SLICED_GRID") && !atoi(getenv("TTS_SLICED_GRID")));
+    if (one_round) p.grid = std::max(1, std::min(p.grid, (num_cu + p.sp.kc - 1) / p.sp.kc));
   }
   return p;
 }
