@@ -113,3 +113,32 @@ def test_chain_streaming_equals_hf():
         final = new
     for c, o in zip(grp, final):
         assert o[:new_n] == c["hf_new"]
+
+
+def test_chain_continuous_batching_equals_hf():
+    """SURVEY §8f rank 3 (vLLM LLM.generate / continuous batching, tts_slots_*): the 8 batch
+    prompts go through 3 persistent decode rows (requests admitted between 16-step chunks as
+    rows free up), and through the vLLM-shaped LLM facade; every request's ids equal
+    transformers' for its prompt, all 500 of them."""
+    from tts_amd.serving import LLM, ContinuousBatcher
+
+    _, _, _, cases = _cases()
+    grp = [c for c in cases if c["group"] == "batch"]
+    m = _lm()
+    new_n = grp[0]["max_length"] - len(grp[0]["prompt"])
+    b = ContinuousBatcher(m, n_slots=3, eos_token_id=grp[0]["eos"], min_new_tokens=grp[0]["min_new"],
+                          repetition_penalty=grp[0]["rep"], chunk=16)
+    got = b.generate([c["prompt"] for c in grp], [new_n] * len(grp))
+    for c, o in zip(grp, got):
+        assert o[:new_n] == c["hf_new"][:new_n], next(i for i, (x, y) in enumerate(zip(o, c["hf_new"])) if x != y)
+
+    class SP:  # vllm.SamplingParams fields the reference sets (inferencing.py:75-92)
+        max_tokens = new_n
+        min_tokens = grp[0]["min_new"]
+        stop_token_ids = [grp[0]["eos"]]
+        repetition_penalty = grp[0]["rep"]
+        temperature = 0.0
+
+    outs = LLM(m, n_slots=4, chunk=16).generate(prompt_token_ids=[c["prompt"] for c in grp[:5]], sampling_params=SP())
+    for c, o in zip(grp[:5], outs):
+        assert list(o.outputs[0].token_ids)[:new_n] == c["hf_new"][:new_n]
