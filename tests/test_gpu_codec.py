@@ -179,3 +179,39 @@ def test_create_from_both_checkpoint_layouts(tmp_path, name, fmt):
     torch.save(src, d2 / "codec.pt")
     with pytest.raises(RuntimeError, match="missing keys"):
         codec.create(str(d2 / "codec.pt"), device=0, max_codes=16)
+
+
+_PASS_CHILD = r'''
+import json, os, sys
+import numpy as np, torch
+sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
+from tts_amd import configs
+from tts_amd.codec import MI355XAudioDecoder
+out = {}
+for name in ("codec-48k", "codec-24k-d2"):
+    dec = MI355XAudioDecoder.synthetic(configs.CODEC_ARCHS[name], seed=11, max_codes=200)
+    rng = np.random.default_rng(7)
+    utts = [rng.integers(0, 65536, size=n) for n in (3, 150, 1, 77, 200, 64, 9)]
+    batch = dec.decode_batch(utts)
+    single = [dec.decode(torch.tensor(u))[0].numpy() for u in utts]
+    out[name] = [bool(np.array_equal(a, b)) for a, b in zip(batch, single)]
+    dec.close()
+print(json.dumps(out))
+'''
+
+
+def test_ragged_batch_in_several_passes_and_two_upsample_stages():
+    """A batch larger than one pass (TTS_CODEC_PASS_CODES=160: the 7 utterances run as 5
+    passes, one of them longer than the pass size) and the 2-stage 48 kHz upsampler over a
+    ragged batch (segment tables at three time resolutions): every utterance equals its
+    single decode bit for bit."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _PASS_CHILD, root], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, TTS_CODEC_PASS_CODES="160"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(res["codec-48k"]) and all(res["codec-24k-d2"]), res
