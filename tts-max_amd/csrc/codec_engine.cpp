@@ -56,6 +56,7 @@ struct Codec {
   DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
   DevBuf meta;   // segment tables, wave offsets, code rows, attention query blocks
   DevBuf planes;  // every GEMM weight (B operand) split once into its bf16 h / m / l planes
+  DevBuf rope_cs;  // [heads][32][cos, sin] of the attention's RoPE
   std::map<const float*, const uint16_t*> bplanes;
   DevBuf codes, wav;  // all utterances' codes; host-bound waveforms staged on the device
 };
@@ -289,6 +290,8 @@ void codec_load(Engine* e, const tts_codec_config* cfgp, const tts_tensor_desc* 
       cd->bplanes[w.first] = p;
       off += (3 * w.second + 127) & ~(size_t)127;
     }
+    cd->rope_cs.alloc((size_t)c.heads * (c.hidden_dim / c.heads / 2) * 2 * 4);
+    launch_codec_rope_table(cd->rope_cs.as<float>(), c.heads, nullptr);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipDeviceSynchronize());
   }
@@ -433,8 +436,9 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
     const CodecTfBlock& tb = cd.tf[l];
     launch_rmsnorm_f32(x, L0.M, D, tb.att_norm, 1e-6f, R(b2, D), s);
     gemm(R(b2, D), L0.M, D, D, tb.c_attn, 3 * D, nullptr, R(qkv, 3 * D), 3 * D, nullptr, 0, s);
-    launch_codec_rope(R(qkv, 3 * D), L0.M, H, D / H, s);
-    launch_codec_attention(qkv, L0.seg, (const int2*)(mb + qb_o), (int)qblk.size(), H, D / H, b2, s);
+    // (RoPE of q and k runs inside the attention kernel's staging)
+    launch_codec_attention(qkv, L0.seg, (const int2*)(mb + qb_o), (int)qblk.size(), H, D / H, cd.rope_cs.as<float>(),
+                           b2, s);
     gemm(R(b2, D), L0.M, D, D, tb.c_proj, D, nullptr, x, D, x, 0, s);
     launch_rmsnorm_f32(x, L0.M, D, tb.ffn_norm, 1e-6f, R(b2, D), s);
     gemm(R(b2, D), L0.M, D, D, tb.fc1, 4 * D, nullptr, R(bigp, 4 * D), 4 * D, nullptr, 1, s);

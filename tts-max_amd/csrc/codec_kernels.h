@@ -54,13 +54,15 @@ void launch_rmsnorm_f32(const float* x, int T, int C, const float* w, float eps,
 // LayerNorm over channels with affine
 void launch_layernorm_f32(const float* x, int T, int C, const float* w, const float* b, float eps,
                           float* y, hipStream_t s);
-// torchtune RoPE applied with position = head index, interleaved pairs, in place on q and k
-void launch_codec_rope(float* qkv, int T, int heads, int hd, hipStream_t s);
-// non-causal full attention within each utterance, fp32, qkv rows [3*heads*hd] -> out rows
-// [heads*hd]; qblk = (utterance, first query) of each 64-query block, codec_attn_qblocks(T) per utterance
+// non-causal full attention within each utterance, fp32, qkv rows [3*heads*hd] (q and k
+// before RoPE: the torchtune rotation with position = head index is applied while staging)
+// -> out rows [heads*hd]; qblk = (utterance, first query) of each 64-query block,
+// codec_attn_qblocks(T) per utterance
 int codec_attn_qblocks(int T);
 void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
-                            int hd, float* out, hipStream_t s);
+                            int hd, const float* rope_cs, float* out, hipStream_t s);
+// rope_cs [heads][hd/2][cos, sin] of that rotation (once, at load)
+void launch_codec_rope_table(float* rope_cs, int heads, hipStream_t s);
 // ConvTranspose1d gather per utterance: y[t'][co] = b[co] + sum_j Z[(t'+pad-j)/u][j*Cout+co]
 void launch_convt_gather(const float* Z, const CodecSeg* seg_in, const CodecSeg* seg_out, int B, int max_To, int Cout,
                          int k, int u, int pad, const float* bias, float* y, hipStream_t s);

@@ -550,32 +550,6 @@ void launch_layernorm_f32(const float* x, int T, int C, const float* w, const fl
   hipLaunchKernelGGL(layernorm_f32_kernel, dim3(T), dim3(256), 0, s, x, C, w, b, eps, y);
 }
 
-// torchtune RotaryPositionalEmbeddings(dim=64, base=10000) as the reference applies it to
-// [b, h, t, d] tensors: the rotated "sequence" index is the HEAD index (decoder_modules.py
-// 276-281; same quirk documented in transformers models/xcodec2).  Pairs are interleaved.
-__global__ void codec_rope_kernel(float* __restrict__ qkv, int T, int heads, int hd) {
-  const int t = blockIdx.x;
-  const int W = heads * hd;
-  for (int i = threadIdx.x; i < heads * hd; i += blockDim.x) {  // one (q or k) pair per 2
-    const int h = i / hd, d = i % hd;
-    if (d & 1) continue;
-    const int pi = d >> 1;
-    const float theta = 1.0f / powf(10000.0f, (float)(2 * pi) / (float)hd);
-    const float ang = (float)h * theta;
-    const float c = cosf(ang), s = sinf(ang);
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {  // q then k
-      float* p = qkv + (size_t)t * 3 * W + r * W + h * hd + d;
-      const float x0 = p[0], x1 = p[1];
-      p[0] = x0 * c - x1 * s;
-      p[1] = x1 * c + x0 * s;
-    }
-  }
-}
-
-void launch_codec_rope(float* qkv, int T, int heads, int hd, hipStream_t s) {
-  hipLaunchKernelGGL(codec_rope_kernel, dim3(T), dim3(256), 0, s, qkv, T, heads, hd);
-}
 
 // ------------------------------------------------------------- codec attention --------
 // Non-causal SDPA (decoder_modules.py:283-285) for head_dim 64 in fp32, as flash attention on
@@ -616,6 +590,23 @@ TTS_DEV f32x4_t mfma_x3(const u32x4_t (&a)[3], const u32x4_t (&b)[3], f32x4_t c)
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf(a[0]), bf(b[0]), c, 0, 0, 0);
 }
 
+// torchtune RotaryPositionalEmbeddings(dim=64, base=10000) as the reference applies it to
+// [b, h, t, d] tensors: the rotated "sequence" index is the HEAD index (decoder_modules.py
+// 276-281; same quirk documented in transformers models/xcodec2), pairs interleaved: the
+// pair (d, d+1) of head h turns by h * 10000^(-d/64).  Applied in the attention kernel's
+// staging to 8 consecutive dims d0 .. d0+7 of q (and, with the same formula, of k).
+// (cos, sin) of every (head, pair) come from a table made once at load (codec_rope_table)
+TTS_DEV void rope8(float (&v)[8], const float2* __restrict__ cs, int d0) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float2 t = cs[(d0 >> 1) + j];
+    const float c = t.x, sn = t.y;
+    const float x0 = v[2 * j], x1 = v[2 * j + 1];
+    v[2 * j] = x0 * c - x1 * sn;
+    v[2 * j + 1] = x1 * c + x0 * sn;
+  }
+}
+
 // max / sum over the 16 lanes of a DPP row (every lane ends with the same bits)
 TTS_DEV float row16_max(float v) {
   v = fmaxf(v, dpp_mov<0xB1>(-INFINITY, v));
@@ -633,6 +624,7 @@ TTS_DEV float row16_sum(float v) {
 __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict__ qkv_all,
                                                          const CodecSeg* __restrict__ seg,
                                                          const int2* __restrict__ qblk, int heads,
+                                                         const float2* __restrict__ rope_cs,
                                                          float* __restrict__ out_all) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ks = (bf16_t*)smem;                 // [3][64 keys][APL]
@@ -662,6 +654,7 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
         const float4 a = p[0], b = p[1];
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
       }
+      rope8(v, rope_cs + h * (AD / 2), kk * 32 + 8 * g);  // (the rotation of q, fused here)
       split3(v, qa[kk][0], qa[kk][1], qa[kk][2]);
     }
   }
@@ -699,12 +692,26 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
       v1[i] = x.y;
     }
   };
+  // the rotation of k (fused): this thread's K units always hold dims (t & 7) * 8 .. +7
+  float kc_[4], ks_[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float2 cs = rope_cs[h * (AD / 2) + ((t & 7) * 8 >> 1) + j];
+    kc_[j] = cs.x;
+    ks_[j] = cs.y;
+  }
   load(0);
   for (int k0 = 0; k0 < T; k0 += AB) {
     __syncthreads();  // the previous chunk's K / V^T reads are done
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int u = t + 256 * it, key = u >> 3, d8 = (u & 7) * 8;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x0 = kreg[it][2 * j], x1 = kreg[it][2 * j + 1];
+        kreg[it][2 * j] = x0 * kc_[j] - x1 * ks_[j];
+        kreg[it][2 * j + 1] = x1 * kc_[j] + x0 * ks_[j];
+      }
       u32x4_t ph, pm, pl;
       split3(kreg[it], ph, pm, pl);
       *(u32x4_t*)(Ks + (0 * 64 + key) * APL + d8) = ph;
@@ -800,10 +807,27 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
 int codec_attn_qblocks(int T) { return (T + AB - 1) / AB; }
 
 void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
-                            int hd, float* out, hipStream_t s) {
+                            int hd, const float* rope_cs, float* out, hipStream_t s) {
   if (hd != AD) throw std::runtime_error("codec attention: head_dim 64 expected");
   dim3 grid(nqblk, heads);
-  hipLaunchKernelGGL(codec_attn_kernel, grid, dim3(256), kAttnLds, s, qkv, seg, qblk, heads, out);
+  hipLaunchKernelGGL(codec_attn_kernel, grid, dim3(256), kAttnLds, s, qkv, seg, qblk, heads, (const float2*)rope_cs,
+                     out);
+}
+
+// (cos, sin) of the torchtune rotation for every (head h, pair p): angle h * 10000^(-2p/64),
+// fp32 as the reference's cache (decoder_modules.py:276-281: position = head index)
+__global__ void codec_rope_table_kernel(float2* cs, int heads) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= heads * (AD / 2)) return;
+  const int h = i / (AD / 2), pi = i % (AD / 2);
+  const float theta = 1.0f / powf(10000.0f, (float)(2 * pi) / (float)AD);
+  const float ang = (float)h * theta;
+  cs[i] = make_float2(cosf(ang), sinf(ang));
+}
+
+void launch_codec_rope_table(float* cs, int heads, hipStream_t s) {
+  hipLaunchKernelGGL(codec_rope_table_kernel, dim3((heads * (AD / 2) + 255) / 256), dim3(256), 0, s, (float2*)cs,
+                     heads);
 }
 
 // ConvTranspose1d(stride u, padding pad) from Z[t][j*Cout + co] = sum_ci x[t][ci] W[ci][co][j]:
