@@ -105,12 +105,13 @@ def _worker(rank, world, port, balance, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("balance", ["contiguous", "lpt"])
-def test_dp_world2_gloo_equals_single(balance):
+@pytest.mark.parametrize("balance,world", [("contiguous", 2), ("lpt", 2), ("contiguous", 12)])
+def test_dp_world2_gloo_equals_single(balance, world):
+    """world 12 > 11 requests: one rank owns nothing and still joins every collective."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, balance, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, balance, q)) for r in range(world)]
     for p in ps:
         p.start()
     out = q.get(timeout=120)
