@@ -31,17 +31,6 @@ int64_t numel(const tts_tensor_desc& d) {
   return n;
 }
 
-static size_t dtype_size(int dt) {
-  switch (dt) {
-    case TTS_DT_F32: return 4;
-    case TTS_DT_BF16: return 2;
-    case TTS_DT_F16: return 2;
-    case TTS_DT_I32: return 4;
-    case TTS_DT_I64: return 8;
-  }
-  return 0;
-}
-
 void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging) {
   const int64_t n = numel(d);
   if (d.dtype == TTS_DT_BF16) {
