@@ -43,7 +43,7 @@ struct DevBuf {
     bytes = n;
   }
   void release() {
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
   }

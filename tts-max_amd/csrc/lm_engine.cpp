@@ -231,7 +231,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
 
   // ---- workspaces
   LmWork& w = e->w;
-  if (w.graph) { hipGraphExecDestroy(w.graph); w.graph = nullptr; w.graph_batch = -1; }
+  if (w.graph) { (void)hipGraphExecDestroy(w.graph); w.graph = nullptr; w.graph_batch = -1; }
   const int B = c.max_batch, S = c.max_seq_len;
   const int R = std::max(B, std::min(kMaxPrefillRows, B * S));
   w.cap_rows = R;
