@@ -35,12 +35,12 @@ static tts_status guarded(F&& f) {
 hipStream_t pick_stream(Engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
 
 Engine::~Engine() {
-  if (w.graph) hipGraphExecDestroy(w.graph);
-  if (w.h_active) hipHostFree(w.h_active);
+  if (w.graph) (void)hipGraphExecDestroy(w.graph);
+  if (w.h_active) (void)hipHostFree(w.h_active);
   if (codec) codec_destroy(codec);
   for (auto& v : ev)
-    if (v) hipEventDestroy(v);
-  if (stream) hipStreamDestroy(stream);
+    if (v) (void)hipEventDestroy(v);
+  if (stream) (void)hipStreamDestroy(stream);
 }
 
 }  // namespace tts
@@ -74,8 +74,8 @@ tts_status tts_engine_create(int32_t device, tts_engine** out) {
 void tts_engine_destroy(tts_engine* e) {
   if (!e) return;
   Engine* E = reinterpret_cast<Engine*>(e);
-  hipSetDevice(E->device);
-  hipDeviceSynchronize();
+  (void)hipSetDevice(E->device);
+  (void)hipDeviceSynchronize();
   delete E;
 }
 

@@ -66,7 +66,6 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
   __shared__ unsigned hist[256];
   __shared__ int s_cnt;
   __shared__ uint32_t s_thr;
-  __shared__ int s_tok;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (a.done && a.done[b]) return;
   const float* l = a.logits + (size_t)b * a.ldl;
@@ -181,7 +180,6 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
       if (acc > u) { pick = i; break; }
     }
     const int tok = (int)(uint32_t)cand[pick];
-    s_tok = tok;
     if (a.probs) {
       for (int i = 0; i < nkeep; ++i) {
         const int id = (int)(uint32_t)cand[i];
