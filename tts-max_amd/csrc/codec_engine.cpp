@@ -377,7 +377,7 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
     wav_off[b] = w;
     w += (long long)seg[NU][b].T * c.hop_length;
     for (int t = 0; t < lens[b]; ++t) code_row.push_back(seg[0][b].row + t);
-    for (int q = 0; q < codec_attn_qblocks(lens[b]); ++q) qblk.push_back(make_int2(b, q * 64));
+    for (int q = 0; q < codec_attn_qblocks(lens[b]); ++q) qblk.push_back(make_int2(b, q * codec_attn_qrows()));
   }
   std::vector<char> host;
   auto put = [&](const void* p, size_t n) {

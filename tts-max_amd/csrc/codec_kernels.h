@@ -59,6 +59,7 @@ void launch_layernorm_f32(const float* x, int T, int C, const float* w, const fl
 // -> out rows [heads*hd]; qblk = (utterance, first query) of each 64-query block,
 // codec_attn_qblocks(T) per utterance
 int codec_attn_qblocks(int T);
+int codec_attn_qrows();  // queries per block (first query of block q = q * codec_attn_qrows())
 void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
                             int hd, const float* rope_cs, float* out, hipStream_t s);
 // rope_cs [heads][hd/2][cos, sin] of that rotation (once, at load)

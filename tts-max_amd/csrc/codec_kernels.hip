@@ -564,7 +564,7 @@ constexpr int AB = 64;        // queries per workgroup / keys per chunk
 constexpr int AD = 64;        // head dim
 constexpr int APL = AB + 8;   // bf16 row stride of the K / V^T planes (144 B: conflict-free b128 reads)
 constexpr int APS = AB + 4;   // fp32 row stride of a wave's P tile
-constexpr size_t kAttnLds = 2 * 3 * 64 * APL * 2 + 4 * 16 * APS * 4;
+constexpr size_t attn_lds(int nw) { return 2 * 3 * 64 * APL * 2 + (size_t)nw * 16 * APS * 4; }
 
 // 8 fp32 -> (h, m, l) bf16x8 planes with h + m + l == x (as split8 in gemm_bx3_kernel)
 TTS_DEV void split3(const float (&v)[8], u32x4_t& h, u32x4_t& m, u32x4_t& l) {
@@ -621,7 +621,9 @@ TTS_DEV float row16_sum(float v) {
   return v + dpp_mov<0x140>(0.f, v);
 }
 
-__global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict__ qkv_all,
+// NW waves = 16 NW queries per workgroup (the K / V^T staging of a chunk is shared by them)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __restrict__ qkv_all,
                                                          const CodecSeg* __restrict__ seg,
                                                          const int2* __restrict__ qblk, int heads,
                                                          const float2* __restrict__ rope_cs,
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ks = (bf16_t*)smem;                 // [3][64 keys][APL]
   bf16_t* Vt = Ks + 3 * 64 * APL;             // [3][64 d][APL]
-  float* Ps = (float*)(Vt + 3 * 64 * APL);    // [4 waves][16][APS]
+  float* Ps = (float*)(Vt + 3 * 64 * APL);    // [NW waves][16][APS]
   // block-diagonal over a ragged batch: (utterance, query block, head), keys of that
   // utterance only
   const int2 qb = qblk[blockIdx.x];
@@ -668,13 +670,15 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  // this thread's share of a chunk: K units (key, 8 d) u = t, t + 256; V^T unit (8 keys, 2 d)
-  const int dp = t & 31, kg = t >> 5;
-  float kreg[2][8], v0[8], v1[8];
+  // this thread's share of a chunk: K units (key, 8 d) u = t, t + 64 NW, ...; one V^T unit
+  // of (8 keys, VD dims)
+  constexpr int NT = 64 * NW, KIT = 512 / NT, VD = 512 / NT;
+  const int dp = t % (64 / VD), kg = t / (64 / VD);
+  float kreg[KIT][8], v0[8], v1[8];
   auto load = [&](int k0) {  // global -> registers (zeros past the utterance's last key)
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int u = t + 256 * it, key = u >> 3, d8 = (u & 7) * 8;
+    for (int it = 0; it < KIT; ++it) {
+      const int u = t + NT * it, key = u >> 3, d8 = (u & 7) * 8;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
       if (k0 + key < T) {
         const float4* p = (const float4*)(qkv + (size_t)(k0 + key) * ld + W + h * AD + d8);
@@ -686,10 +690,16 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float2 x = make_float2(0.f, 0.f);
-      if (k0 + 8 * kg + i < T) x = *(const float2*)(qkv + (size_t)(k0 + 8 * kg + i) * ld + 2 * W + h * AD + 2 * dp);
-      v0[i] = x.x;
-      v1[i] = x.y;
+      const bool in = k0 + 8 * kg + i < T;
+      const float* vp = qkv + (size_t)(k0 + 8 * kg + i) * ld + 2 * W + h * AD + VD * dp;
+      if constexpr (VD == 2) {
+        float2 x = make_float2(0.f, 0.f);
+        if (in) x = *(const float2*)vp;
+        v0[i] = x.x;
+        v1[i] = x.y;
+      } else {
+        v0[i] = in ? *vp : 0.f;
+      }
     }
   };
   // the rotation of k (fused): this thread's K units always hold dims (t & 7) * 8 .. +7
@@ -704,8 +714,8 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
   for (int k0 = 0; k0 < T; k0 += AB) {
     __syncthreads();  // the previous chunk's K / V^T reads are done
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int u = t + 256 * it, key = u >> 3, d8 = (u & 7) * 8;
+    for (int it = 0; it < KIT; ++it) {
+      const int u = t + NT * it, key = u >> 3, d8 = (u & 7) * 8;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float x0 = kreg[it][2 * j], x1 = kreg[it][2 * j + 1];
@@ -721,13 +731,15 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
     {
       u32x4_t ph, pm, pl;
       split3(v0, ph, pm, pl);
-      *(u32x4_t*)(Vt + (0 * 64 + 2 * dp) * APL + 8 * kg) = ph;
-      *(u32x4_t*)(Vt + (1 * 64 + 2 * dp) * APL + 8 * kg) = pm;
-      *(u32x4_t*)(Vt + (2 * 64 + 2 * dp) * APL + 8 * kg) = pl;
-      split3(v1, ph, pm, pl);
-      *(u32x4_t*)(Vt + (0 * 64 + 2 * dp + 1) * APL + 8 * kg) = ph;
-      *(u32x4_t*)(Vt + (1 * 64 + 2 * dp + 1) * APL + 8 * kg) = pm;
-      *(u32x4_t*)(Vt + (2 * 64 + 2 * dp + 1) * APL + 8 * kg) = pl;
+      *(u32x4_t*)(Vt + (0 * 64 + VD * dp) * APL + 8 * kg) = ph;
+      *(u32x4_t*)(Vt + (1 * 64 + VD * dp) * APL + 8 * kg) = pm;
+      *(u32x4_t*)(Vt + (2 * 64 + VD * dp) * APL + 8 * kg) = pl;
+      if constexpr (VD == 2) {
+        split3(v1, ph, pm, pl);
+        *(u32x4_t*)(Vt + (0 * 64 + 2 * dp + 1) * APL + 8 * kg) = ph;
+        *(u32x4_t*)(Vt + (1 * 64 + 2 * dp + 1) * APL + 8 * kg) = pm;
+        *(u32x4_t*)(Vt + (2 * 64 + 2 * dp + 1) * APL + 8 * kg) = pl;
+      }
     }
     __syncthreads();
     if (k0 + AB < T) load(k0 + AB);  // next chunk in flight during this chunk's math
@@ -804,14 +816,24 @@ __global__ __launch_bounds__(256) void codec_attn_kernel(const float* __restrict
   }
 }
 
-int codec_attn_qblocks(int T) { return (T + AB - 1) / AB; }
+// queries per workgroup: 64 (4 waves) or 128 (8 waves: TTS_CODEC_ATTN_W=8)
+static int attn_waves() {
+  static const int w = (getenv("TTS_CODEC_ATTN_W") && atoi(getenv("TTS_CODEC_ATTN_W")) == 8) ? 8 : 4;
+  return w;
+}
+int codec_attn_qrows() { return 16 * attn_waves(); }
+int codec_attn_qblocks(int T) { return (T + codec_attn_qrows() - 1) / codec_attn_qrows(); }
 
 void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
                             int hd, const float* rope_cs, float* out, hipStream_t s) {
   if (hd != AD) throw std::runtime_error("codec attention: head_dim 64 expected");
   dim3 grid(nqblk, heads);
-  hipLaunchKernelGGL(codec_attn_kernel, grid, dim3(256), kAttnLds, s, qkv, seg, qblk, heads, (const float2*)rope_cs,
-                     out);
+  if (attn_waves() == 8)
+    hipLaunchKernelGGL(codec_attn_kernel<8>, grid, dim3(512), attn_lds(8), s, qkv, seg, qblk, heads,
+                       (const float2*)rope_cs, out);
+  else
+    hipLaunchKernelGGL(codec_attn_kernel<4>, grid, dim3(256), attn_lds(4), s, qkv, seg, qblk, heads,
+                       (const float2*)rope_cs, out);
 }
 
 // (cos, sin) of the torchtune rotation for every (head h, pair p): angle h * 10000^(-2p/64),
