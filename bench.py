@@ -157,6 +157,17 @@ def main():
     audio_s = N / carch.token_rate  # seconds of audio per utterance
     rtf = (elapsed / args.steps) / audio_s  # wall per utterance-batch / audio seconds (per GPU)
 
+    # ---- the codec leg alone (B utterances of prompt + N codes, one ragged pass), after the timed region
+    rngc = np.random.default_rng(7)
+    uttsc = [rngc.integers(0, 65536, size=codes_per_utt).tolist() for _ in range(B)]
+    dec.decode_batch(uttsc, out=wav_buf)
+    torch.cuda.synchronize()
+    tc = time.perf_counter()
+    for _ in range(3):
+        dec.decode_batch(uttsc, out=wav_buf)
+    torch.cuda.synchronize()
+    codec_ms = (time.perf_counter() - tc) / 3 * 1000
+
     # ---- roofline of the dominant kernel (and the whole decode step), live HIP events
     kern = {}
     ctx_mid = P + N // 2
@@ -225,9 +236,20 @@ def main():
         torch.cuda.synchronize()
         e32 = (time.perf_counter() - t) / reps
         a32, b32, k32 = lm.last_timing()
+        # the codec leg alone: the same 32 utterances of prompt + N codes as one ragged pass
+        rng32 = np.random.default_rng(32)
+        utts32 = [rng32.integers(0, 65536, size=codes_per_utt).tolist() for _ in range(32)]
+        dec.decode_batch(utts32, out=wav_buf)
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        for _ in range(3):
+            dec.decode_batch(utts32, out=wav_buf)
+        torch.cuda.synchronize()
+        codec32_ms = (time.perf_counter() - tc) / 3 * 1000
         sec["bs32"] = dict(value=round(n32 / reps / e32, 2), unit="audio-codes/s", ms_per_step=round(1000 * e32, 3),
                            x_realtime=round(32 * N / carch.token_rate / e32, 2), lm_prefill_ms=round(a32, 3),
-                           lm_decode_ms=round(b32, 3), decode_step_ms=round(b32 / max(k32, 1), 4))
+                           lm_decode_ms=round(b32, 3), decode_step_ms=round(b32 / max(k32, 1), 4),
+                           codec_ms=round(codec32_ms, 3), codec_utterances=32, codec_codes_per_utterance=codes_per_utt)
         # the 32-row decode kernels: live HIP-event time, algorithmic bytes, PMC HBM traffic
         k32s = {}
         for k in lm.KERNELS:
@@ -278,6 +300,7 @@ def main():
             "x_realtime": round(1.0 / rtf * B, 2),
             "lm_prefill_ms": round(lm_prefill / args.steps, 3),
             "lm_decode_ms": round(lm_decode / args.steps, 3),
+            "codec_ms": round(codec_ms, 3),
             "config": {
                 "workload": f"{arch.name} bf16 bs={B}/GPU: prompt {P} tokens ({args.prompt_codes} codes), "
                             f"{N} greedy codes, codec {carch.name} on {codes_per_utt} codes",
