@@ -135,6 +135,10 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   p.grid = p.sp.grid;
   const int w = p.sp.waves, ks = p.sp.ksplit;
   p.a_lds = wgemm_lds_bytes(w, ks, ng, M, K, true) <= kLdsBudget;
+  // experiment hook: TTS_HEAD_GRID=<workgroups> for the lm_head launch (units are walked
+  // grid-stride, so any grid covers them; at most LOGITS_MAX_PARTS argmax partials)
+  static const int head_grid = getenv("TTS_HEAD_GRID") ? atoi(getenv("TTS_HEAD_GRID")) : 0;
+  if (epi == EPI_LOGITS && head_grid > 0) p.grid = std::min(head_grid, LOGITS_MAX_PARTS);
   // Up to 16 rows, a residual projection whose rows do not fit the LDS prologue and whose
   // K-sliced form would run the grid in more than two rounds (TTS-1-Max down, K 14336: 7
   // chunks x 256 workgroups) streams its A fragments from L2 beside the weights (A_GLOBAL
