@@ -1035,9 +1035,12 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   const double act_rw = 2.0 * rows;
   // launches rotate over the layers (as the decode step does), so a layer's weights are
   // not still cached from the previous launch: the timing reflects HBM streaming
+  // (experiment hook TTS_BENCH_ONE_LAYER=1: every launch on layer 0, weights L2-warm when
+  // they fit the XCDs' L2s — what a cross-kernel weight prefetch could at best buy)
+  static const bool one_layer = getenv("TTS_BENCH_ONE_LAYER") && atoi(getenv("TTS_BENCH_ONE_LAYER"));
   int it_layer = 0;
   auto launch = [&]() {
-    const int li = it_layer++ % c.num_layers;
+    const int li = one_layer ? 0 : it_layer++ % c.num_layers;
     const LmLayer& ly = X.M.layers[li];
     switch (which) {
       case 0:
