@@ -189,6 +189,14 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
  * Both produce identical ids. */
 tts_status tts_lm_decode_path(tts_engine* e, int32_t* persistent);
 
+/* The lm_head's exponent-coded weight stream (lossless: the same bf16 operands, 25 % fewer
+ * bytes per coded tile; lm_wcomp.hip) used by the one-row-tile (<= 16 rows) lm_head
+ * launches.  on: 1 build it (once) and use it, 0 stream the plain tiles (the default;
+ * TTS_WCOMP=1 at load: coded), -1 leave as is.  Outputs (optional): coded tiles (0 until
+ * built), escaped (raw) tiles, exponent base eb.  Ids are identical either way; measured
+ * slower than the plain stream on MI355X, hence opt-in. */
+tts_status tts_lm_coded_weights(tts_engine* e, int32_t on, int64_t* ntiles, int64_t* nesc, int32_t* eb);
+
 /* Times one decode-step kernel of the loaded model in isolation (HIP events on the engine
  * stream around `iters` back-to-back launches, after one warm-up launch) for roofline
  * accounting.  which: 0 qkv projection (+RMSNorm), 1 o_proj (+residual), 2 gate/up

@@ -122,6 +122,64 @@ void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::ve
 }
 }  // namespace
 
+// Exponent-coded copy of a tiled matrix (lm_wcomp.hip).  eb = the window [eb, eb + 15] of
+// bf16 exponent fields that holds the most tiles whole (a histogram of the tiles' (min, max)
+// exponent pairs); the other tiles are escaped raw, slots in tile order (deterministic).
+// Opt-in (TTS_WCOMP=1 at load, or tts_lm_coded_weights): measured slower than the plain
+// stream (lm_head 120 -> 141-149 us; 125 us with the decode skipped).
+bool wcomp_enabled() {
+  static const bool v = getenv("TTS_WCOMP") && atoi(getenv("TTS_WCOMP"));
+  return v;
+}
+
+void lm_build_coded_head(Engine* e) {
+  LmModel& M = e->lm;
+  if (M.head_c.ntiles > 0) return;
+  HIP_CHECK(hipStreamSynchronize(e->stream));
+  build_wcomp(M.lm_head, (long long)M.cfg.vocab_size * M.cfg.hidden_size / 512, M.head_c, e->stream);
+  M.wc_dummy.alloc(256);
+  HIP_CHECK(hipMemsetAsync(M.wc_dummy.p, 0, 256, e->stream));
+  HIP_CHECK(hipStreamSynchronize(e->stream));
+}
+
+void build_wcomp(const bf16_t* tiled, long long ntiles, LmModel::WComp& wc, hipStream_t s) {
+  DevBuf st;
+  st.alloc((size_t)ntiles * 2);
+  uint8_t* emin = st.as<uint8_t>();
+  uint8_t* emax = emin + ntiles;
+  launch_wcomp_stats(tiled, ntiles, emin, emax, s);
+  HIP_CHECK(hipGetLastError());
+  std::vector<uint8_t> lo(ntiles), hi(ntiles);
+  HIP_CHECK(hipMemcpyAsync(lo.data(), emin, ntiles, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(hi.data(), emax, ntiles, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<long long> hist(256 * 256, 0);
+  for (long long t = 0; t < ntiles; ++t) ++hist[lo[t] * 256 + hi[t]];
+  long long best = -1;
+  uint32_t eb = 0;
+  for (int b = 0; b <= 240; ++b) {
+    long long n = 0;
+    for (int l = b; l <= b + 15; ++l)
+      for (int h = l; h <= b + 15; ++h) n += hist[l * 256 + h];
+    if (n > best) { best = n; eb = (uint32_t)b; }
+  }
+  std::vector<uint32_t> meta(ntiles);
+  long long nesc = 0;
+  for (long long t = 0; t < ntiles; ++t)
+    meta[t] = (lo[t] >= eb && hi[t] <= eb + 15) ? 0u : (uint32_t)(++nesc);
+  TTS_REQUIRE(nesc < (1ll << 31), "coded weight stream: too many escaped tiles");
+  wc.meta.alloc((size_t)ntiles * 4);
+  wc.rec.alloc((size_t)ntiles * 768);
+  wc.esc.alloc((size_t)std::max(1ll, nesc) * 1024);
+  HIP_CHECK(hipMemcpyAsync(wc.meta.p, meta.data(), (size_t)ntiles * 4, hipMemcpyHostToDevice, s));
+  launch_wcomp_encode(tiled, ntiles, eb, wc.meta.as<uint32_t>(), wc.rec.as<uint32_t>(), wc.esc.as<bf16_t>(), s);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(s));
+  wc.eb = eb;
+  wc.ntiles = ntiles;
+  wc.nesc = nesc;
+}
+
 // the persistent step's hand-off state: granule tags 0xffffffff and flags 0 (never a step's
 // tag), step tag 1
 void persist_reset(Engine* e, hipStream_t s) {
@@ -220,6 +278,13 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
     HIP_CHECK(hipMemcpy(M.rope.as<bf16_t>(), cs.data(), cs.size() * 2, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(M.rope.as<bf16_t>() + cs.size(), sn.data(), sn.size() * 2,
                         hipMemcpyHostToDevice));
+  }
+  M.head_c.ntiles = 0;
+  M.use_wc = false;
+  M.head_c.rec.release(); M.head_c.meta.release(); M.head_c.esc.release();
+  if (wcomp_enabled()) {
+    lm_build_coded_head(e);
+    M.use_wc = true;
   }
   M.id_to_code.clear();
   if (tm.has("vocab.id_to_code")) {
@@ -386,6 +451,12 @@ struct Ctx {
       }
       a.x = xin; a.M = m; a.K = K; a.ldx = K;
       a.w = W; a.N = N;
+      const LmModel::WComp* wc = (W == M.lm_head && epi == EPI_LOGITS) ? &M.head_c : nullptr;
+      if (wc && M.use_wc && wc->ntiles > 0 && m <= 16) {  // (launch_wgemm uses it for one-row-tile launches)
+        a.wc_rec = wc->rec.as<uint32_t>(); a.wc_meta = wc->meta.as<uint32_t>();
+        a.wc_esc = wc->esc.as<bf16_t>(); a.wc_dummy = M.wc_dummy.as<uint32_t>();
+        a.wc_eb2 = (wc->eb << 7) | (wc->eb << 23);
+      }
       a.normw = normw; a.eps = c.rms_norm_eps;
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;

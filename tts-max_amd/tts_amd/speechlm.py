@@ -330,6 +330,14 @@ class MI355XSpeechLM:
         _lib.check(self._lib.tts_lm_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value
 
+    def coded_weights(self, on: bool | None = None) -> dict:
+        """The lm_head's exponent-coded (lossless, 12-bit) weight stream: switch it on / off for
+        the one-row-tile launches (None: leave as is) and report its tiles / escaped tiles / eb."""
+        nt, ne, eb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        flag = -1 if on is None else int(bool(on))
+        _lib.check(self._lib.tts_lm_coded_weights(self._h, flag, ctypes.byref(nt), ctypes.byref(ne), ctypes.byref(eb)))
+        return {"tiles": nt.value, "escaped": ne.value, "eb": eb.value}
+
     KERNELS = ("qkv", "o_proj", "gate_up", "down", "lm_head", "attention")
 
     def bench_kernel(self, which: str, rows: int = 1, ctx: int = 450, iters: int = 50) -> tuple[float, float]:
