@@ -82,7 +82,6 @@ struct LmModel {
   };
   WComp head_c;       // lm_head
   bool use_wc = false;  // one-row-tile lm_head launches stream head_c (tts_lm_coded_weights)
-  DevBuf wc_dummy;    // 64 zero dwords (the spare load of a coded tile)
   int qkv_n() const { return (cfg.num_heads + 2 * cfg.num_kv_heads) * cfg.head_dim; }
 };
 

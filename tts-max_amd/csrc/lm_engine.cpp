@@ -137,8 +137,6 @@ void lm_build_coded_head(Engine* e) {
   if (M.head_c.ntiles > 0) return;
   HIP_CHECK(hipStreamSynchronize(e->stream));
   build_wcomp(M.lm_head, (long long)M.cfg.vocab_size * M.cfg.hidden_size / 512, M.head_c, e->stream);
-  M.wc_dummy.alloc(256);
-  HIP_CHECK(hipMemsetAsync(M.wc_dummy.p, 0, 256, e->stream));
   HIP_CHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -454,7 +452,7 @@ struct Ctx {
       const LmModel::WComp* wc = (W == M.lm_head && epi == EPI_LOGITS) ? &M.head_c : nullptr;
       if (wc && M.use_wc && wc->ntiles > 0 && m <= 16) {  // (launch_wgemm uses it for one-row-tile launches)
         a.wc_rec = wc->rec.as<uint32_t>(); a.wc_meta = wc->meta.as<uint32_t>();
-        a.wc_esc = wc->esc.as<bf16_t>(); a.wc_dummy = M.wc_dummy.as<uint32_t>();
+        a.wc_esc = wc->esc.as<bf16_t>();
         a.wc_eb2 = (wc->eb << 7) | (wc->eb << 23);
       }
       a.normw = normw; a.eps = c.rms_norm_eps;

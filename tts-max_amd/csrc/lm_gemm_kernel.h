@@ -899,7 +899,7 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   // epilogues built with it; the plain tiles stay for every other launch)
   constexpr bool cw_built = EPI == EPI_LOGITS;
   if (cw_built && mt == 1 && a.wc_rec && !a.sliced && !a.fattn_wgs) {
-    if (!a.wc_meta || !a.wc_esc || !a.wc_dummy) throw std::runtime_error("wgemm: incomplete coded weight stream");
+    if (!a.wc_meta || !a.wc_esc) throw std::runtime_error("wgemm: incomplete coded weight stream");
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY, cw_built>), g,
                        dim3(WAVES * 64), lds, s, a);
   } else if (mt == 1)

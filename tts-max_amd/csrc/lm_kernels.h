@@ -114,7 +114,6 @@ struct WgemmArgs {
   const uint32_t* wc_rec = nullptr;    // [tiles][64 lanes][3] u32
   const uint32_t* wc_meta = nullptr;   // [tiles]
   const bf16_t* wc_esc = nullptr;      // [escaped tiles][512] (the tile's own layout)
-  const uint32_t* wc_dummy = nullptr;  // 64 dwords: the spare load of a coded tile
   uint32_t wc_eb2 = 0;                 // (eb << 7) | (eb << 23)
 };
 
