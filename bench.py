@@ -72,7 +72,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # TTS_BENCH_DIST=1: the RCCL (torchrun) path even at one rank — rehearses the driver's
+    # multi-GPU run (broadcast, per-rank shard, gather of codes and waveforms, MAX/SUM
+    # all-reduce) on a one-GPU box
+    if world > 1 or os.environ.get("TTS_BENCH_DIST") == "1":
         import torch.distributed as dist  # noqa: F811
 
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
