@@ -231,6 +231,8 @@ tts_status tts_lm_coded_weights(tts_engine* e, int32_t on, int64_t* ntiles, int6
     Engine* E = reinterpret_cast<Engine*>(e);
     TTS_REQUIRE(E->lm.loaded, "no model loaded");
     TTS_REQUIRE(on >= -1 && on <= 1, "on must be -1, 0 or 1");
+    TTS_REQUIRE(on < 0 || (!E->gen.open && !E->slots.open),
+                "cannot switch the weight stream while a generation or slot batch is open");
     HIP_CHECK(hipSetDevice(E->device));
     if (on == 1) lm_build_coded_head(E);
     if (on >= 0 && (on == 1) != E->lm.use_wc) {

@@ -278,6 +278,8 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
                         hipMemcpyHostToDevice));
   }
   M.head_c.ntiles = 0;
+  M.head_c.nesc = 0;
+  M.head_c.eb = 0;
   M.use_wc = false;
   M.head_c.rec.release(); M.head_c.meta.release(); M.head_c.esc.release();
   if (wcomp_enabled()) {
