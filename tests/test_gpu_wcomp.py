@@ -112,3 +112,15 @@ def test_lm_head_coded_equals_plain_ids():
         eight = m.generate_batch(prompts, max_length=120, repetition_penalty=1.1)
         res.setdefault(on, []).append((one, eight))
     assert res[True][0] == res[False][0] == res[True][1]
+    # switching under an open generation is refused (the captured step holds the operands);
+    # the generation then finishes with the stream it started with
+    from tts_amd import _lib
+
+    it = m.generate_stream(prompts[:1], max_length=120, chunk=20, repetition_penalty=1.1)
+    next(it)
+    with pytest.raises(_lib.TtsError):
+        m.coded_weights(False)
+    last = None
+    for last in it:
+        pass
+    assert last[0] == res[True][0][0]
