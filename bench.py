@@ -13,11 +13,15 @@ batch 1 per GPU, P = 200 (150 prompt codes), N = 500 codes (10 s of audio), code
 (hop 160, ups [3]) on 650 codes.  Random-init weights of that architecture (no checkpoint
 is reachable offline); synthetic token ids of the reference prompt shape.
 
-Multi-GPU (torchrun): one process per GPU (tts_amd/dp.py synthesize_sharded).  Rank 0
-builds the request batch and broadcasts it over RCCL; each rank generates and voices its
-contiguous shard (the reference's rank partition, quality_validation.py:171-182); codes
-and waveforms are gathered back to rank 0 (the only exchange steps of the path).  Weak
-scaling.
+Multi-GPU: one process per GPU (tts_amd/dp.py synthesize_sharded).  `--gpus N` without a
+launcher spawns the N ranks itself (tts_amd/launch.py; the parent never touches the GPU);
+under torchrun the ranks come from the environment.  Rank 0 builds the request batch and
+broadcasts it over RCCL; each rank generates and voices its contiguous shard (the
+reference's rank partition, quality_validation.py:171-182); codes and waveforms are
+gathered back to rank 0 (the only exchange steps of the path).  Weak scaling.
+
+Named workloads (--workload): config2 = the default above; config3 = TTS-1 32 utterances
+per GPU; config4 = TTS-1-Max 8 utterances per GPU (BASELINE configs[3]: bs=64 over 8 GPUs).
 
 Prints ONE JSON line (rank 0).
 """
@@ -42,6 +46,10 @@ MODEL_NAMES = {"tts1": "TTS-1 (Llama-3.2-1B dims, V=193856, tied)",
                "tts1-max": "TTS-1-Max (Llama-3.1-8B dims, V=193856, untied)"}
 
 
+# BASELINE.json configs by name: (arch, utterances per GPU)
+WORKLOADS = {"config2": ("tts1", 1), "config3": ("tts1", 32), "config4": ("tts1-max", 8)}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -62,7 +70,19 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=30)
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the N=1 secondary lines (bs=32 batched decode, bs=8 streaming latency)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="named BASELINE workload (sets --arch / --batch per GPU)")
     args = ap.parse_args()
+    if args.workload:
+        args.arch, args.batch = WORKLOADS[args.workload]
+
+    from tts_amd import launch
+
+    if launch.needs_spawn(args.gpus):
+        # one process per GPU: spawn the ranks before anything initialises HIP here
+        # (torch.cuda.device_count() does not), rank 0 prints the line
+        sys.exit(launch.spawn(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              torch.cuda.device_count()))
 
     from tts_amd import configs, dp, synth
     from tts_amd.codec import MI355XAudioDecoder
@@ -97,7 +117,7 @@ def main():
 
     max_seq = P + N + 16
     t0 = time.time()
-    secondary = (world == 1 and not args.no_secondary)
+    secondary = (world == 1 and not args.no_secondary and args.arch == "tts1" and B == 1)
     lm = MI355XSpeechLM.synthetic(arch, seed=0x5EED, device=local, max_batch=max(B, 32 if secondary else 1),
                                   max_seq_len=max_seq)
     dec = MI355XAudioDecoder.synthetic(carch, seed=0xC0DEC, device=local, max_codes=args.prompt_codes + N + 8)
@@ -185,17 +205,9 @@ def main():
         fused = True
     except Exception:  # noqa: BLE001 (not this shape: separate launches)
         pass
-    # the one-row step as one persistent launch over all layers (lm_persist.hip)
-    persist = B == 1 and lm.decode_persistent()
-    if persist:
-        ms, by = lm.bench_kernel("persist", rows=1, ctx=ctx_mid, iters=max(3, args.kernel_iters // 3))
-        kern["persist"] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
-    # per-step share: the layer kernels once per layer (or the persistent launch once), lm_head once
-    if persist:
-        in_step = ["persist", "lm_head"]
-    else:
-        in_step = [k for k in kern if not (fused and k in ("qkv", "attention")) and k != "persist"]
-    share = {k: kern[k]["avg_ms"] * (1 if k in ("lm_head", "persist") else arch.num_layers) for k in in_step}
+    # per-step share: the layer kernels once per layer, lm_head once
+    in_step = [k for k in kern if not (fused and k in ("qkv", "attention"))]
+    share = {k: kern[k]["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k in in_step}
     dom = max(share, key=share.get)
     step_ms = lm_decode / max(dec_steps, 1)
     kv_ctx_bytes = B * arch.kv_bytes_per_token() * ctx_mid
@@ -214,7 +226,7 @@ def main():
         return round(json.load(open(hits[-1]))["hbm_bytes_per_launch"]), os.path.relpath(hits[-1], ROOT)
 
     traffic, traffic_src = pmc(dom, B)
-    kname = {"attention": "attn_decode", "persist": "persist_step (all layers, one launch)"}.get(dom, f"wgemm/{dom}")
+    kname = {"attention": "attn_decode"}.get(dom, f"wgemm/{dom}")
     roofline = dict(bound="hbm", kernel=kname,
                     achieved=round(kern[dom]["gbs"], 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(kern[dom]["gbs"] / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
@@ -350,49 +362,69 @@ def cpu_baseline(arch, carch, prompt, N, args):
     calls, tts/inference/inferencing.py:94-107: bf16, greedy, repetition penalty 1.1,
     min_new_tokens) on the same synthetic weights — prefill of the same prompt + `cpu_steps`
     generated codes — and the codec as the fp32 port (oracle/codec_oracle.py; the reference
-    codec cannot travel to the box) on a proportional number of codes; scaled to codes/s of
-    the full job."""
+    codec cannot travel to the box) on the whole utterance (prompt + N codes, no
+    extrapolation); the LM decode is scaled to the N-code job.
+
+    Threads: torch.set_num_threads at every core the process may run on (the affinity
+    count), and at 16 (the box's CPU share per GPU) beside it; the faster
+    is `value`, with the thread count that won in `cores`."""
     from oracle import codec_oracle
     from oracle.hf_ref import hf_model
     from tts_amd import configs, synth
 
-    threads = torch.get_num_threads()
     cpu_model, ncpu, avail = _cpu_info()
     t0 = time.time()
     model = hf_model(arch, synth.lm_weights_cpu(arch, 0x5EED))
-    log(f"cpu baseline: transformers model ready in {time.time() - t0:.1f}s, {threads} threads ({cpu_model})")
-    S = args.cpu_steps
+    log(f"cpu baseline: transformers model ready in {time.time() - t0:.1f}s ({cpu_model}, affinity {avail})")
     ids = torch.tensor([prompt])
-    with torch.no_grad():
-        t1 = time.perf_counter()
-        model(ids)  # prefill alone (its time is subtracted from the generate call below)
-        t_prefill = time.perf_counter() - t1
-        t2 = time.perf_counter()
-        out = model.generate(input_ids=ids, max_length=len(prompt) + S, min_new_tokens=S,
-                             eos_token_id=configs.vocab_for(arch).speech_end_id, do_sample=False,
-                             repetition_penalty=1.1)
-        t_gen = time.perf_counter() - t2
-    assert out.shape[1] == len(prompt) + S
-    t_dec = max(t_gen - t_prefill, 1e-9) / (S - 1)  # the first new token comes from the prefill
+    eos = configs.vocab_for(arch).speech_end_id
+    saved = torch.get_num_threads()
+
+    def lm_leg(threads, S):
+        torch.set_num_threads(threads)
+        with torch.no_grad():
+            model(ids[:, :16])  # thread-pool warm-up
+            t1 = time.perf_counter()
+            model(ids)  # prefill alone (its time is subtracted from the generate call below)
+            t_prefill = time.perf_counter() - t1
+            t2 = time.perf_counter()
+            out = model.generate(input_ids=ids, max_length=len(prompt) + S, min_new_tokens=S,
+                                 eos_token_id=eos, do_sample=False, repetition_penalty=1.1)
+            t_gen = time.perf_counter() - t2
+        assert out.shape[1] == len(prompt) + S
+        return t_prefill, max(t_gen - t_prefill, 1e-9) / (S - 1)  # the first new token comes from the prefill
+
+    legs = {}
+    for threads in sorted({avail, 16}):
+        # the all-core leg may oversubscribe the box's CPU share: a shorter sample
+        S = args.cpu_steps if threads <= 16 else max(16, args.cpu_steps // 4)
+        legs[threads] = (S,) + lm_leg(threads, S)
+        log(f"cpu baseline: {threads} threads: prefill {legs[threads][1]:.2f}s, {legs[threads][2] * 1000:.1f} ms/code")
+    best = min(legs, key=lambda t: legs[t][1] + (N - 1) * legs[t][2])
     del model
+    torch.set_num_threads(best)
     cw = synth.codec_weights_cpu(carch, 0xC0DEC)
-    T_s = 65
+    T_s = args.prompt_codes + N
     t3 = time.perf_counter()
     codec_oracle.decode(cw, torch.randint(0, 65536, (T_s,)), carch.hop_length, carch.upsample_factors,
                         carch.kernel_sizes, carch.depth)
-    t_codec_per_code = (time.perf_counter() - t3) / T_s
-    full = t_prefill + (N - 1) * t_dec + (args.prompt_codes + N) * t_codec_per_code
+    t_codec = time.perf_counter() - t3
+    torch.set_num_threads(saved)
+    S, t_prefill, t_dec = legs[best]
+    full = t_prefill + (N - 1) * t_dec + t_codec
     return {
         "value": round(N / full, 3),
         "unit": "audio-codes/s",
-        "cores": threads,
+        "cores": best,
         "kind": "reference",
-        "cpu": {"model": cpu_model, "nproc": ncpu, "affinity": avail, "torch_threads": threads},
+        "cpu": {"model": cpu_model, "nproc": ncpu, "affinity": avail},
+        "by_threads": {str(t): {"codes_per_s": round(N / (v[1] + (N - 1) * v[2] + t_codec), 3),
+                                "prefill_s": round(v[1], 3), "ms_per_code": round(1000 * v[2], 2),
+                                "sample_codes": v[0]} for t, v in legs.items()},
         "sample": (f"transformers {__import__('transformers').__version__} LlamaForCausalLM.generate (bf16, greedy, "
-                   f"rep 1.1; the reference's LM call) on the same weights: prefill {len(prompt)} tokens "
-                   f"({t_prefill:.2f}s) + {S} generated codes ({t_dec * 1000:.1f} ms/code), codec as the fp32 port "
-                   f"on {T_s} codes ({t_codec_per_code * 1000:.2f} ms/code); extrapolated to the {N}-code job "
-                   f"+ {args.prompt_codes + N}-code codec"),
+                   f"rep 1.1; the reference's LM call) on the same weights at {best} threads: prefill {len(prompt)} "
+                   f"tokens ({t_prefill:.2f}s) + {S} generated codes ({t_dec * 1000:.1f} ms/code), extrapolated to "
+                   f"{N} codes; codec as the fp32 port on the whole {T_s}-code utterance ({t_codec:.2f}s)"),
     }
 
 

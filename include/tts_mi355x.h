@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TTS_ABI_VERSION 2
+#define TTS_ABI_VERSION 3
 
 typedef int32_t tts_status;
 enum {
@@ -183,27 +183,12 @@ tts_status tts_lm_id_to_code(tts_engine* e, const int32_t* ids, int32_t n, int32
 tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms,
                               int32_t* decode_steps);
 
-/* Which form the loaded model's one-row decode step takes: *persistent = 1 when it runs as
- * ONE persistent launch over all layers (lm_persist.hip: TTS-1 geometry on 256 CUs,
- * max_seq_len <= 1024, TTS_PERSIST=1), 0 when it runs as per-layer launches (the default).
- * Both produce identical ids. */
-tts_status tts_lm_decode_path(tts_engine* e, int32_t* persistent);
-
-/* The lm_head's exponent-coded weight stream (lossless: the same bf16 operands, 25 % fewer
- * bytes per coded tile; lm_wcomp.hip) used by the one-row-tile (<= 16 rows) lm_head
- * launches.  on: 1 build it (once) and use it, 0 stream the plain tiles (the default;
- * TTS_WCOMP=1 at load: coded), -1 leave as is.  Outputs (optional): coded tiles (0 until
- * built), escaped (raw) tiles, exponent base eb.  Ids are identical either way; measured
- * slower than the plain stream on MI355X, hence opt-in. */
-tts_status tts_lm_coded_weights(tts_engine* e, int32_t on, int64_t* ntiles, int64_t* nesc, int32_t* eb);
-
 /* Times one decode-step kernel of the loaded model in isolation (HIP events on the engine
  * stream around `iters` back-to-back launches, after one warm-up launch) for roofline
  * accounting.  which: 0 qkv projection (+RMSNorm), 1 o_proj (+residual), 2 gate/up
  * (+RMSNorm, SwiGLU), 3 down_proj (+residual), 4 lm_head (+RMSNorm, penalty, argmax
  * partials), 5 decode attention (ctx = `ctx` positions), 6 qkv with the decode attention
- * fused in (one row), 7 the persistent one-row step over all layers (rows = 1; see
- * tts_lm_decode_path).  rows = batch rows.
+ * fused in (one row).  rows = batch rows.
  * Outputs: average ms per launch and the algorithmic HBM bytes one launch must move. */
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes);

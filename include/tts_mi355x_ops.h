@@ -25,12 +25,6 @@ tts_status tts_synth_fill(void* dst, int32_t dtype, int64_t n, uint64_t seed, fl
  * 2 (SwiGLU) takes W = [gate; up] ([N/2][K] each) and interleaves their n-tiles. */
 tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, int32_t epi, void* stream);
 
-/* Exponent-coded stream of `ntiles` 1 KiB tiles (lm_wcomp.hip) built from w_tiled and
- * decoded back into out (same size): out == w_tiled bit for bit.  eb / nesc (optional):
- * the chosen exponent window base and the count of escaped (raw) tiles.  Synchronous. */
-tts_status tts_op_wcomp_roundtrip(const void* w_tiled, int64_t ntiles, void* out, int32_t* eb, int64_t* nesc,
-                                  void* stream);
-
 /* y[M][ldo] (bf16) = epilogue( A[M][K] . W^T ), A optionally RMSNorm'ed with normw.
  * epi: 0 store, 1 residual (resid += y, in place), 2 SwiGLU (W = interleaved gate/up tiles,
  * N = 2*intermediate, output [M][N/2]).  M <= 64. */

@@ -218,37 +218,6 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
   });
 }
 
-tts_status tts_lm_decode_path(tts_engine* e, int32_t* persistent) {
-  return guarded([&] {
-    TTS_REQUIRE(e && persistent, "null argument");
-    *persistent = lm_decode_persistent(reinterpret_cast<Engine*>(e)) ? 1 : 0;
-  });
-}
-
-tts_status tts_lm_coded_weights(tts_engine* e, int32_t on, int64_t* ntiles, int64_t* nesc, int32_t* eb) {
-  return guarded([&] {
-    TTS_REQUIRE(e, "null engine");
-    Engine* E = reinterpret_cast<Engine*>(e);
-    TTS_REQUIRE(E->lm.loaded, "no model loaded");
-    TTS_REQUIRE(on >= -1 && on <= 1, "on must be -1, 0 or 1");
-    TTS_REQUIRE(on < 0 || (!E->gen.open && !E->slots.open),
-                "cannot switch the weight stream while a generation or slot batch is open");
-    HIP_CHECK(hipSetDevice(E->device));
-    if (on == 1) lm_build_coded_head(E);
-    if (on >= 0 && (on == 1) != E->lm.use_wc) {
-      E->lm.use_wc = on == 1;
-      if (E->w.graph) {  // the captured step holds the old operands
-        (void)hipGraphExecDestroy(E->w.graph);
-        E->w.graph = nullptr;
-        E->w.graph_batch = -1;
-      }
-    }
-    if (ntiles) *ntiles = E->lm.head_c.ntiles;
-    if (nesc) *nesc = E->lm.head_c.nesc;
-    if (eb) *eb = (int32_t)E->lm.head_c.eb;
-  });
-}
-
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes) {
   return guarded([&] {
@@ -306,22 +275,6 @@ static int device_cu_count() {  // (single-device process: cached, no per-call q
     HIP_CHECK(hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
   return num_cu;
-}
-
-tts_status tts_op_wcomp_roundtrip(const void* w_tiled, int64_t ntiles, void* out, int32_t* eb, int64_t* nesc,
-                                  void* stream) {
-  return guarded([&] {
-    TTS_REQUIRE(w_tiled && out && ntiles >= 1, "bad argument");
-    hipStream_t s = (hipStream_t)stream;
-    LmModel::WComp wc;
-    build_wcomp((const bf16_t*)w_tiled, ntiles, wc, s);
-    launch_wcomp_decode(wc.rec.as<uint32_t>(), wc.meta.as<uint32_t>(), wc.esc.as<bf16_t>(), wc.eb, ntiles,
-                        (bf16_t*)out, s);
-    HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipStreamSynchronize(s));
-    if (eb) *eb = (int32_t)wc.eb;
-    if (nesc) *nesc = wc.nesc;
-  });
 }
 
 tts_status tts_op_retile(const void* w, void* w_tiled, int32_t N, int32_t K, int32_t epi, void* stream) {

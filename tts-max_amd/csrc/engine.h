@@ -73,15 +73,6 @@ struct LmModel {
   bf16_t* final_norm = nullptr;
   bf16_t* lm_head = nullptr;  // tiled [V][hidden]
   std::vector<int> id_to_code;  // host LUT (optional)
-  // exponent-coded copy of a tiled matrix for the one-row launches (lm_wcomp.hip); the plain
-  // tiles stay for prefill and batched rows
-  struct WComp {
-    DevBuf rec, meta, esc;
-    uint32_t eb = 0;
-    long long ntiles = 0, nesc = 0;
-  };
-  WComp head_c;       // lm_head
-  bool use_wc = false;  // one-row-tile lm_head launches stream head_c (tts_lm_coded_weights)
   int qkv_n() const { return (cfg.num_heads + 2 * cfg.num_kv_heads) * cfg.head_dim; }
 };
 
@@ -93,9 +84,6 @@ struct LmWork {
   DevBuf x, xn, qkv, attn_out, act, q_rot, last_x;  // activations
   DevBuf part_o, part_ml;                           // attention split partials
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
-  DevBuf pgran, pflags, pseq;                       // persistent one-row step: granules, flags, tag
-  bool persist_ok = false;                          // the geometry runs the persistent step
-  int persist_ur[4] = {0, 0, 0, 0};
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
@@ -169,11 +157,8 @@ void lm_slots_read(Engine* e, int slot, int32_t* out_ids, int cap, int32_t* n_ou
 void lm_slots_release(Engine* e, int slot);
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
               float* logits, hipStream_t s);
-void build_wcomp(const bf16_t* tiled, long long ntiles, LmModel::WComp& wc, hipStream_t s);
-void lm_build_coded_head(Engine* e);  // the lm_head's coded stream, once
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes);
-bool lm_decode_persistent(Engine* e);
 
 // upload a named tensor to device memory as bf16 (convert from f32 if needed)
 void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging);

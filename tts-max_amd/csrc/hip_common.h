@@ -110,18 +110,3 @@ TTS_DEV float block_max(float v, float* red) {
 
 TTS_DEV float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
-// Exponent-coded bf16 (lm_wcomp.hip): a lane's 8 values as {d0, d1, n}: byte j of d0|d1 =
-// sign << 7 | mantissa (7 bits) of value j, n holds code c = exponent - eb of value 2q at bits
-// 4q..4q+3 and of value 2q+1 at bits 16+4q..16+4q+3.  Dword q of the bf16 fragment: the byte
-// pair spread to both bytes of each half (v_perm), masked to sign + mantissa, plus the code
-// placed at the exponent field, plus eb there (eb + c <= 255: no carry reaches the sign).
-typedef __attribute__((ext_vector_type(3))) unsigned int u32x3_t;
-TTS_DEV u32x4_t wc_decode(u32x4_t r, uint32_t eb2) {
-  const uint32_t d0 = r.x, d1 = r.y, n = r.z;
-  u32x4_t o;
-  o.x = (__builtin_amdgcn_perm(0u, d0, 0x01010000u) & 0x807F807Fu) + ((n & 0x000F000Fu) << 7) + eb2;
-  o.y = (__builtin_amdgcn_perm(0u, d0, 0x03030202u) & 0x807F807Fu) + ((n & 0x00F000F0u) << 3) + eb2;
-  o.z = (__builtin_amdgcn_perm(0u, d1, 0x01010000u) & 0x807F807Fu) + ((n & 0x0F000F00u) >> 1) + eb2;
-  o.w = (__builtin_amdgcn_perm(0u, d1, 0x03030202u) & 0x807F807Fu) + ((n & 0xF000F000u) >> 5) + eb2;
-  return o;
-}

@@ -206,174 +206,6 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   }
 }
 
-// Decode-step attention (one new query row per sequence), K/V appended in place.
-// Chunk = 4 waves x IT iterations x (64 / (D/8)) positions.  Every K and V load of the
-// chunk is issued at kernel entry, before the RoPE work, so the chunk costs one memory
-// round trip; the scores / softmax / P.V then run from registers and LDS.
-template <int D, int IT>
-__global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
-  constexpr int LPP = D / 8;     // lanes per position (16 B each)
-  constexpr int PPW = 64 / LPP;  // positions per wave-instruction
-  constexpr int PPB = 4 * PPW;   // positions per block iteration
-  constexpr int SPLIT = PPB * IT;
-  __shared__ float qs[GQA * D];
-  __shared__ float kn[D], vn[D];
-  __shared__ float s[GQA * SPLIT];
-  __shared__ float ml[2 * GQA];
-  __shared__ float ored[4 * GQA * D];
-  const int nrk = a.rows * a.KVH, nb = nrk * a.nsplit;
-  if ((int)blockIdx.x >= nb) return;
-  const int rk = blockIdx.x % nrk, sp = blockIdx.x / nrk;
-  const int row = rk / a.KVH, kvh = rk % a.KVH;
-  const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
-  const int t0 = sp * SPLIT;
-  if (t0 >= ctx) return;
-  const int t1 = min(t0 + SPLIT, ctx);
-  const int n = t1 - t0;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane % LPP, pg = lane / LPP;
-  const size_t cbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
-  const bf16_t* kc = a.kcache + cbase;
-  const bf16_t* vc = a.vcache + cbase;
-
-  u32x4_t kr[IT], vr[IT];
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int t = t0 + it * PPB + wave * PPW + pg;
-    if (t < t1 && t != pos) {
-      kr[it] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
-      vr[it] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
-    } else {
-      kr[it] = u32x4_t{0u, 0u, 0u, 0u};
-      vr[it] = u32x4_t{0u, 0u, 0u, 0u};
-    }
-  }
-
-  const bool has_new = pos >= t0 && pos < t1;
-  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
-  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
-  for (int i = threadIdx.x; i < GQA * D; i += blockDim.x) {
-    const int g = i / D, d = i % D, h = kvh * GQA + g;
-    qs[i] = rope_elem<D>(a.qkv + (size_t)row * a.ld_qkv + h * D, d, cosr, sinr);
-  }
-  if (has_new) {
-    const bf16_t* kin = a.qkv + (size_t)row * a.ld_qkv + a.H * D + kvh * D;
-    const bf16_t* vin = kin + a.KVH * D;
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-      const float kr2 = rope_elem<D>(kin, d, cosr, sinr);
-      kn[d] = kr2;
-      vn[d] = bf2f(vin[d]);
-      a.kcache[cbase + (size_t)pos * D + d] = f2bf(kr2);
-      a.vcache[cbase + (size_t)pos * D + d] = vin[d];
-    }
-  }
-  __syncthreads();
-
-  float qr[GQA][8];
-#pragma unroll
-  for (int g = 0; g < GQA; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qr[g][j] = qs[g * D + c * 8 + j];
-
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int t = t0 + it * PPB + wave * PPW + pg;
-    float kv[8];
-    if (t == pos) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kv[j] = kn[c * 8 + j];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) { kv[2 * q] = bf_lo(kr[it][q]); kv[2 * q + 1] = bf_hi(kr[it][q]); }
-    }
-    float part[GQA];
-#pragma unroll
-    for (int g = 0; g < GQA; ++g) {
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc += qr[g][j] * kv[j];
-      part[g] = acc;
-    }
-#pragma unroll
-    for (int o = 1; o < LPP; o <<= 1)
-#pragma unroll
-      for (int g = 0; g < GQA; ++g) part[g] += __shfl_xor(part[g], o, 64);
-    if (c == 0 && t < t1) {
-#pragma unroll
-      for (int g = 0; g < GQA; ++g) s[g * SPLIT + (t - t0)] = part[g] * a.scale;
-    }
-  }
-  __syncthreads();
-  for (int g = wave; g < GQA; g += 4) {
-    float m = -INFINITY;
-    for (int i = lane; i < n; i += 64) m = fmaxf(m, s[g * SPLIT + i]);
-    m = wave_max(m);
-    float l = 0.f;
-    for (int i = lane; i < n; i += 64) {
-      const float p = expf(s[g * SPLIT + i] - m);
-      s[g * SPLIT + i] = rbf(p);  // flash numerics: bf16 P into P.V, fp32 normaliser
-      l += p;
-    }
-    l = wave_sum(l);
-    if (lane == 0) { ml[2 * g] = m; ml[2 * g + 1] = l; }
-  }
-  __syncthreads();
-  float o[GQA][8];
-#pragma unroll
-  for (int g = 0; g < GQA; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int t = t0 + it * PPB + wave * PPW + pg;
-    if (t < t1) {
-      float vv[8];
-      if (t == pos) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) vv[j] = vn[c * 8 + j];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { vv[2 * q] = bf_lo(vr[it][q]); vv[2 * q + 1] = bf_hi(vr[it][q]); }
-      }
-#pragma unroll
-      for (int g = 0; g < GQA; ++g) {
-        const float p = s[g * SPLIT + (t - t0)];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] += p * vv[j];
-      }
-    }
-  }
-#pragma unroll
-  for (int off = LPP; off < 64; off <<= 1)
-#pragma unroll
-    for (int g = 0; g < GQA; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[g][j] += __shfl_xor(o[g][j], off, 64);
-  if (pg == 0) {
-#pragma unroll
-    for (int g = 0; g < GQA; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ored[(wave * GQA + g) * D + c * 8 + j] = o[g][j];
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < GQA * D; i += blockDim.x) {
-    const int g = i / D, d = i % D, h = kvh * GQA + g;
-    const float sum = ored[(0 * GQA + g) * D + d] + ored[(1 * GQA + g) * D + d] +
-                      ored[(2 * GQA + g) * D + d] + ored[(3 * GQA + g) * D + d];
-    const size_t pidx = ((size_t)row * a.H + h) * a.nsplit + sp;
-    a.part_o[pidx * D + d] = sum;
-    if (d == 0) { a.part_ml[pidx * 2] = ml[2 * g]; a.part_ml[pidx * 2 + 1] = ml[2 * g + 1]; }
-  }
-}
-
-// (superseded by lm_attn_decode.hip: the lane-shuffle reductions above lower to
-//  ds_bpermute and serialise on LDS latency; kept only for reference / A-B runs)
-void launch_attn_decode_step_shfl(const AttnArgs& a, hipStream_t s) {
-  dim3 grid(a.rows * a.KVH * a.nsplit);
-  if (a.D == 64) hipLaunchKernelGGL((attn_decode_kernel<64, 4>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((attn_decode_kernel<128, 4>), grid, dim3(256), 0, s, a);
-}
-
 template <int D>
 __global__ void attn_combine_kernel(AttnArgs a) {
   const int row = blockIdx.x / a.H, h = blockIdx.x % a.H;

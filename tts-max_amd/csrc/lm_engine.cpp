@@ -17,7 +17,6 @@
 #include <cstdio>
 
 #include "engine.h"
-#include "lm_persist.h"
 
 namespace tts {
 
@@ -122,73 +121,6 @@ void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::ve
 }
 }  // namespace
 
-// Exponent-coded copy of a tiled matrix (lm_wcomp.hip).  eb = the window [eb, eb + 15] of
-// bf16 exponent fields that holds the most tiles whole (a histogram of the tiles' (min, max)
-// exponent pairs); the other tiles are escaped raw, slots in tile order (deterministic).
-// Opt-in (TTS_WCOMP=1 at load, or tts_lm_coded_weights): measured slower than the plain
-// stream (lm_head 120 -> 141-149 us; 125 us with the decode skipped).
-bool wcomp_enabled() {
-  static const bool v = getenv("TTS_WCOMP") && atoi(getenv("TTS_WCOMP"));
-  return v;
-}
-
-void lm_build_coded_head(Engine* e) {
-  LmModel& M = e->lm;
-  if (M.head_c.ntiles > 0) return;
-  HIP_CHECK(hipStreamSynchronize(e->stream));
-  build_wcomp(M.lm_head, (long long)M.cfg.vocab_size * M.cfg.hidden_size / 512, M.head_c, e->stream);
-  HIP_CHECK(hipStreamSynchronize(e->stream));
-}
-
-void build_wcomp(const bf16_t* tiled, long long ntiles, LmModel::WComp& wc, hipStream_t s) {
-  DevBuf st;
-  st.alloc((size_t)ntiles * 2);
-  uint8_t* emin = st.as<uint8_t>();
-  uint8_t* emax = emin + ntiles;
-  launch_wcomp_stats(tiled, ntiles, emin, emax, s);
-  HIP_CHECK(hipGetLastError());
-  std::vector<uint8_t> lo(ntiles), hi(ntiles);
-  HIP_CHECK(hipMemcpyAsync(lo.data(), emin, ntiles, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(hi.data(), emax, ntiles, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  std::vector<long long> hist(256 * 256, 0);
-  for (long long t = 0; t < ntiles; ++t) ++hist[lo[t] * 256 + hi[t]];
-  long long best = -1;
-  uint32_t eb = 0;
-  for (int b = 0; b <= 240; ++b) {
-    long long n = 0;
-    for (int l = b; l <= b + 15; ++l)
-      for (int h = l; h <= b + 15; ++h) n += hist[l * 256 + h];
-    if (n > best) { best = n; eb = (uint32_t)b; }
-  }
-  std::vector<uint32_t> meta(ntiles);
-  long long nesc = 0;
-  for (long long t = 0; t < ntiles; ++t)
-    meta[t] = (lo[t] >= eb && hi[t] <= eb + 15) ? 0u : (uint32_t)(++nesc);
-  TTS_REQUIRE(nesc < (1ll << 31), "coded weight stream: too many escaped tiles");
-  wc.meta.alloc((size_t)ntiles * 4);
-  wc.rec.alloc((size_t)ntiles * 768);
-  wc.esc.alloc((size_t)std::max(1ll, nesc) * 1024);
-  HIP_CHECK(hipMemcpyAsync(wc.meta.p, meta.data(), (size_t)ntiles * 4, hipMemcpyHostToDevice, s));
-  launch_wcomp_encode(tiled, ntiles, eb, wc.meta.as<uint32_t>(), wc.rec.as<uint32_t>(), wc.esc.as<bf16_t>(), s);
-  HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipStreamSynchronize(s));
-  wc.eb = eb;
-  wc.ntiles = ntiles;
-  wc.nesc = nesc;
-}
-
-// the persistent step's hand-off state: granule tags 0xffffffff and flags 0 (never a step's
-// tag), step tag 1
-void persist_reset(Engine* e, hipStream_t s) {
-  LmWork& w = e->w;
-  HIP_CHECK(hipMemsetAsync(w.pgran.p, 0xff, w.pgran.bytes, s));
-  HIP_CHECK(hipMemsetAsync(w.pflags.p, 0, w.pflags.bytes, s));
-  const int one = 1;
-  HIP_CHECK(hipMemcpyAsync(w.pseq.p, &one, 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-}
-
 void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int n) {
   TTS_REQUIRE(cfgp != nullptr, "null config");
   const tts_lm_config c = *cfgp;
@@ -277,15 +209,6 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
     HIP_CHECK(hipMemcpy(M.rope.as<bf16_t>() + cs.size(), sn.data(), sn.size() * 2,
                         hipMemcpyHostToDevice));
   }
-  M.head_c.ntiles = 0;
-  M.head_c.nesc = 0;
-  M.head_c.eb = 0;
-  M.use_wc = false;
-  M.head_c.rec.release(); M.head_c.meta.release(); M.head_c.esc.release();
-  if (wcomp_enabled()) {
-    lm_build_coded_head(e);
-    M.use_wc = true;
-  }
   M.id_to_code.clear();
   if (tm.has("vocab.id_to_code")) {
     const tts_tensor_desc& d = tm.get("vocab.id_to_code", {V});
@@ -322,15 +245,6 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
-  w.persist_ok = persist_supported(HID, H, KVH, D, FF, L, S, w.nsplit_decode, w.split_decode, e->num_cu,
-                                   w.persist_ur);
-  if (w.persist_ok) {
-    w.pgran.alloc(persist_gran_elems(L) * 8);
-    w.pflags.alloc(persist_flag_elems(L) * 4);
-    w.pseq.alloc(64);
-    persist_init();
-    persist_reset(e, s);
-  }
   {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
     const int kmax = std::max(HID, std::max(FF, H * D));
     w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
@@ -354,27 +268,10 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
 // ------------------------------------------------------------------------ compute -----
 namespace {
 
-// Decode attention form: chunked kernel (32 workgroups per row at 450 positions) whose
-// partials the o_proj prologue merges (default), or one workgroup per (row, kv head) that
-// merges in LDS (TTS_ATTN_MERGED=1; measured 2x slower at batch 1: 8 CUs stream the KV).
-bool use_split_attn() {
-  static const bool v = !(getenv("TTS_ATTN_MERGED") && atoi(getenv("TTS_ATTN_MERGED")));
-  return v;
-}
-
 // Decode attention of a one-row step fused into the QKV launch (lm_gemm_kernel.h,
 // fattn_consumer): default on; TTS_FUSED_ATTN=0 keeps the separate attention launch.
 bool use_fused_attn() {
   static const bool v = !(getenv("TTS_FUSED_ATTN") && !atoi(getenv("TTS_FUSED_ATTN")));
-  return v;
-}
-
-// The one-row decode step as one persistent launch (lm_persist.hip) where the geometry
-// allows it: opt-in (TTS_PERSIST=1; bit-identical ids).  Measured 45 us per layer against
-// the per-layer launches' 40 (the hand-offs into streaming CUs cost ~2.5 us
-// each and the LDS rings hold only a third of a layer), so the launches stay the default.
-bool use_persist() {
-  static const bool v = getenv("TTS_PERSIST") && atoi(getenv("TTS_PERSIST"));
   return v;
 }
 
@@ -451,12 +348,6 @@ struct Ctx {
       }
       a.x = xin; a.M = m; a.K = K; a.ldx = K;
       a.w = W; a.N = N;
-      const LmModel::WComp* wc = (W == M.lm_head && epi == EPI_LOGITS) ? &M.head_c : nullptr;
-      if (wc && M.use_wc && wc->ntiles > 0 && m <= 16) {  // (launch_wgemm uses it for one-row-tile launches)
-        a.wc_rec = wc->rec.as<uint32_t>(); a.wc_meta = wc->meta.as<uint32_t>();
-        a.wc_esc = wc->esc.as<bf16_t>();
-        a.wc_eb2 = (wc->eb << 7) | (wc->eb << 23);
-      }
       a.normw = normw; a.eps = c.rms_norm_eps;
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
@@ -494,7 +385,7 @@ struct Ctx {
   // The one-row decode step's QKV launch carries the attention (TTS-1 geometry: head dim 64,
   // decode chunks of 128 positions); consecutive fused launches differ in (pos, layer)
   bool fused_attn_ok(int rows, bool decode) const {
-    return decode && rows == 1 && use_fused_attn() && use_split_attn() && c.head_dim == 64 &&
+    return decode && rows == 1 && use_fused_attn() && c.head_dim == 64 &&
            w.split_decode == 128 && c.num_layers >= 2 && c.num_layers <= 64 &&
            wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
   }
@@ -508,43 +399,9 @@ struct Ctx {
     return fx;
   }
 
-  unsigned long long* trace = nullptr;  // diagnostics (lm_bench_kernel, TTS_PERSIST_TRACE)
-
-  void persist_step(const int* slot, const int* pos) {
-    PersistArgs pa;
-    TTS_REQUIRE(c.num_layers <= PersistArgs::kMaxLayers, "persistent step: too many layers");
-    for (int l = 0; l < c.num_layers; ++l) {
-      const LmLayer& ly = M.layers[l];
-      pa.w[l][0] = ly.wqkv; pa.w[l][1] = ly.wo; pa.w[l][2] = ly.wgu; pa.w[l][3] = ly.wd;
-      pa.ln[l][0] = ly.ln1; pa.ln[l][1] = ly.ln2;
-    }
-    pa.L = c.num_layers;
-    pa.x = w.x.as<bf16_t>();
-    pa.row_slot = slot; pa.row_pos = pos;
-    pa.kv = w.kv.as<bf16_t>();
-    pa.kv_layer = (long long)c.max_batch * c.num_kv_heads * c.max_seq_len * c.head_dim;
-    pa.max_seq = c.max_seq_len;
-    pa.rope_cos = M.rope.as<bf16_t>();
-    pa.rope_sin = pa.rope_cos + (size_t)c.max_seq_len * c.head_dim;
-    pa.scale = (float)(1.0 / sqrt((double)c.head_dim));
-    pa.eps = c.rms_norm_eps;
-    pa.NS = w.nsplit_decode;
-    pa.gran = w.pgran.as<uint64_t>();
-    pa.flags = w.pflags.as<int>();
-    pa.err = w.ferr.as<int>();
-    pa.seq = w.pseq.as<int>();
-    pa.ur_qkv = w.persist_ur[0]; pa.ur_o = w.persist_ur[1]; pa.ur_gu = w.persist_ur[2]; pa.ur_d = w.persist_ur[3];
-    pa.trace = trace;
-    launch_persist_step(pa, s);
-  }
-
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
-    if (decode && rows == 1 && w.persist_ok && use_persist()) {
-      persist_step(slot, pos);
-      return;
-    }
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
     for (int l = 0; l < c.num_layers; ++l) {
@@ -558,16 +415,12 @@ struct Ctx {
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE);
       }
-      // decode: the chunked kernel whose partials the o_proj prologue merges (default), or one
-      // workgroup per (row, kv head) that attends and merges (TTS_ATTN_MERGED=1)
-      const bool split_attn = use_split_attn();
+      // decode: the chunked kernel whose partials the o_proj prologue merges
       // (rows <= 16: the merge scratch + A rows fit LDS beside the split-K partials)
-      const bool fuse_combine = decode && split_attn && rows <= 16 &&
+      const bool fuse_combine = decode && rows <= 16 &&
                                 wgemm_oproj_merge_ok(rows, HID, HD, w.nsplit_decode, e->num_cu);
       if (fattn) {
         // (attention ran inside the QKV launch)
-      } else if (decode && !split_attn) {
-        launch_attn_decode_merged(a, s);
       } else if (decode) {
         launch_attn_decode_step(a, s);
       } else {
@@ -580,7 +433,7 @@ struct Ctx {
         exo.attn_split = a.split; exo.attn_nsplit = a.nsplit; exo.attn_D = a.D;
         gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &exo);
       } else {
-        if (!decode || split_attn) launch_attn_combine(a, s);
+        launch_attn_combine(a, s);
         gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
              w.x.as<bf16_t>(), EPI_RESID);
       }
@@ -848,9 +701,8 @@ int lm_gen_continue(Engine* e, int n_steps) {
   return G.finished ? 1 : 0;
 }
 
-// A fused QKV+attention launch (or persistent step) whose granule wait timed out leaves
-// garbage: fail loudly at the next read (the flag and the persistent step's hand-off state
-// are cleared for the next generation).
+// A fused QKV+attention launch whose granule wait timed out leaves garbage: fail loudly at
+// the next read (the flag is cleared for the next generation).
 static void check_fattn(Engine* e, hipStream_t s) {
   if (!e->w.ferr.p) return;
   int err = 0;
@@ -858,7 +710,6 @@ static void check_fattn(Engine* e, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
   if (err) {
     HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 4, s));
-    if (e->w.persist_ok) persist_reset(e, s);
     HIP_CHECK(hipStreamSynchronize(s));
     TTS_REQUIRE(false, "fused QKV+attention: a granule wait timed out (results invalid)");
   }
@@ -1059,16 +910,13 @@ void lm_slots_release(Engine* e, int slot) {
   Z.busy[slot] = 0;
 }
 
-bool lm_decode_persistent(Engine* e) { return e->lm.loaded && e->w.persist_ok && use_persist(); }
-
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which >= 0 && which <= 6 && iters >= 1, "bad kernel selector");
   TTS_REQUIRE(which != 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
-  TTS_REQUIRE(which != 7 || (rows == 1 && lm_decode_persistent(e)), "the persistent step needs one row (TTS-1 geometry)");
   hipStream_t s = e->stream;
   Ctx X(e, s);
   const tts_lm_config& c = X.c;
@@ -1097,7 +945,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   ex.part_stride = LOGITS_MAX_PARTS;
   // attention chunk partials for the fused o_proj prologue
   launch_attn_decode_step(aa, s);
-  const bool fuse_o = use_split_attn() && rows <= 16 &&
+  const bool fuse_o = rows <= 16 &&
                       wgemm_oproj_merge_ok(rows, HID, HD, e->w.nsplit_decode, e->num_cu);
   WgemmArgs exo;
   exo.attn_o = aa.part_o; exo.attn_ml = aa.part_ml; exo.attn_pos = e->w.row_pos.as<int>();
@@ -1141,8 +989,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         b = 2.0 * V * HID + act_rw * HID + 2.0 * HID + rows * (V / 8.0);
         break;
       case 5:
-        if (use_split_attn()) launch_attn_decode_step(aa, s);
-        else launch_attn_decode_merged(aa, s);
+        launch_attn_decode_step(aa, s);
         b = (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2 + act_rw * QKV;
         break;
       case 6: {  // QKV with the decode attention fused in (the one-row decode step's form)
@@ -1154,13 +1001,6 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
             (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2;
         break;
       }
-      case 7:  // every layer of the one-row step as the persistent launch: all layers' weights,
-               // the K/V of ctx positions per layer, the new position's K/V, the row in / out
-        X.persist_step(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
-        b = (double)c.num_layers * (2.0 * (QKV * HID + HID * HD + 2.0 * FF * HID + HID * FF) + 4.0 * HID +
-                                    (double)c.num_kv_heads * (ctx + 1) * c.head_dim * 2 * 2) +
-            act_rw * 2 * HID;
-        break;
     }
   };
   launch();
@@ -1174,27 +1014,6 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   *avg_ms = ms / iters;
   *bytes = b;
   check_fattn(e, s);
-  // diagnostics: TTS_PERSIST_TRACE=<file> writes one traced persistent step's phase
-  // timestamps ([256][L][32] u64, 100 MHz clock) after the timed launches
-  const char* tf = getenv("TTS_PERSIST_TRACE");
-  if (which == 7 && tf && *tf) {
-    DevBuf tb;
-    const size_t n = (size_t)256 * c.num_layers * 32;
-    tb.alloc(n * 8);
-    HIP_CHECK(hipMemsetAsync(tb.p, 0, n * 8, s));
-    X.trace = tb.as<unsigned long long>();
-    X.persist_step(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
-    X.trace = nullptr;
-    std::vector<unsigned long long> h(n);
-    HIP_CHECK(hipMemcpyAsync(h.data(), tb.p, n * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    FILE* f = fopen(tf, "wb");
-    if (f) {
-      fwrite(h.data(), 8, n, f);
-      fclose(f);
-    }
-    check_fattn(e, s);
-  }
 }
 
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,

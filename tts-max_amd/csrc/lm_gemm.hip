@@ -70,10 +70,7 @@ StreamPlan stream_plan(int N, int K, int ng, int num_cu) {
   const int KT = K / 32;
   int c;
   if (ng == 2) c = 5;
-  else if (units >= 4 * num_cu) {
-    static const bool ku16 = getenv("TTS_HEAD_KU16") && atoi(getenv("TTS_HEAD_KU16"));
-    c = ku16 ? 7 : 0;
-  }
+  else if (units >= 4 * num_cu) c = 0;
   else if (K >= 4096) c = 3;
   else c = 2;
   // experiment hook (scripts/wgemm_probe.cpp): TTS_STREAM_PLAN=<shape index>[,grid]

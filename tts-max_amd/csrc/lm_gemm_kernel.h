@@ -178,10 +178,8 @@ TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
 constexpr int A_GLOBAL = 0, A_LDS = 1, A_ATTN = 2;
 
 // MT_MAX: compile-time bound on 16-row m-tiles (1 for decode, 4 for up to 64 rows)
-// CW: the weights come as the exponent-coded stream (a.wc_*, lm_wcomp.hip), decoded in
-// registers to the same bf16 fragments.
 template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R,
-          bool EARLY, bool CW = false>
+          bool EARLY>
 __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
@@ -228,21 +226,6 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     return (long long)r * ur * KT * NG + (((long long)(st + st_off) * nr + ui) * KSPLIT + kpart) * NG * KU;
   };
   const int S = a.sliced ? Sc : kc * Sc;  // stages per item in this launch
-  // CW: lane i < NG*KU of mr[j] = meta word of tile i of the stage ring slot j issues next;
-  // the first R stages' words are loaded before anything else (the stream waits on them),
-  // later ones ride a ring depth ahead of their stage (issue)
-  constexpr int TPS = NG * KU;
-  uint32_t mr[R] = {}, esm[R] = {};
-  int mpu = blockIdx.x * UPW + ugrp, mps = 0;
-  auto mload = [&]() -> uint32_t {
-    const long long t = stile(mpu, mps);
-    if (++mps == S) { mps = 0; mpu += ustride; }
-    return a.wc_meta[t + min(lane, TPS - 1)];
-  };
-  if constexpr (CW) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) { mr[j] = mload(); esm[j] = 0; }
-  }
 
   // ---- operands of the prologue and epilogue are loaded FIRST, the weight stream after:
   // vmcnt retires in issue order, so anything issued behind the stream could not be used
@@ -361,39 +344,12 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // per-iteration condition): every path then has a fixed load count and the compiler's
   // vmcnt waits stay exact (a conditional issue makes it merge paths pessimistically,
   // i.e. drain the ring at every stage).
-  auto issue = [&](u32x4_t (&dst)[KU][NG], u32x4_t (&adst)[KU][AGR ? MT_MAX : 1], uint32_t& mrj,
-                   uint32_t& esmj) {
-    if constexpr (CW) {
-      // coded tile: 12 B per lane + a spare dword from an L2-resident line; escaped
-      // tile: its raw 16 B as the same two loads from the side buffer.  Wave-uniform selects,
-      // a fixed load count (exact vmcnt waits).
-      const long long tb = stile(pu, ps);
-      uint32_t m = 0;
+  auto issue = [&](u32x4_t (&dst)[KU][NG], u32x4_t (&adst)[KU][AGR ? MT_MAX : 1]) {
+    const u32x4_t* q = sptr(pu, ps);
 #pragma unroll
-      for (int kk = 0; kk < KU; ++kk)
+    for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const int i = g * KU + kk;
-          const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)mrj, i);
-          const char* p3 = e ? (const char*)a.wc_esc + (size_t)(e - 1) * 1024 + lane * 16
-                             : (const char*)a.wc_rec + (size_t)(tb + i) * 768 + lane * 12;
-          // (the spare load of a coded tile re-reads this stage's meta words: an L2-hot line
-          // that differs per stage, so the spare loads spread over the L2 channels)
-          const uint32_t* p1 = e ? (const uint32_t*)(p3 + 12) : a.wc_meta + tb + (lane & (TPS - 1));
-          const u32x3_t v = __builtin_nontemporal_load((const u32x3_t*)p3);
-          const uint32_t x = *p1;
-          dst[kk][g] = u32x4_t{v.x, v.y, v.z, x};
-          m |= (e ? 1u : 0u) << i;
-        }
-      esmj = m;
-      mrj = mload();
-    } else {
-      const u32x4_t* q = sptr(pu, ps);
-#pragma unroll
-      for (int kk = 0; kk < KU; ++kk)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) dst[kk][g] = __builtin_nontemporal_load(q + (g * KU + kk) * 64);
-    }
+      for (int g = 0; g < NG; ++g) dst[kk][g] = __builtin_nontemporal_load(q + (g * KU + kk) * 64);
     if constexpr (AGR) {
       const int sg = ps + st_off, ch = kc == 1 ? 0 : sg / Sc;
       const int kt = ch * KTc + kpart * kt_pc + (sg - ch * Sc) * KU - kt_base;
@@ -415,7 +371,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // (unconditional: a wave with no unit streams unit units-1, never consumed (sptr clamps).
   // A branch here would make every prologue wait below drain the primed stages as well)
 #pragma unroll
-  for (int j = 0; j < R; ++j) issue(wr[j], ar[j], mr[j], esm[j]);
+  for (int j = 0; j < R; ++j) issue(wr[j], ar[j]);
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
@@ -666,8 +622,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
       for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    auto consume = [&](const u32x4_t (&src)[KU][NG], const u32x4_t (&asrc)[KU][AGR ? MT_MAX : 1], int stage,
-                       uint32_t esmj) {
+    auto consume = [&](const u32x4_t (&src)[KU][NG], const u32x4_t (&asrc)[KU][AGR ? MT_MAX : 1], int stage) {
       const int sg = stage + st_off, ch = kc == 1 ? 0 : sg / Sc;
       const int kt = ch * KTc + kpart * kt_pc + (sg - ch * Sc) * KU - kt_base;  // A column tile
 #pragma unroll
@@ -683,32 +638,15 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           const bf16x8_t af = as_bf16x8(av);
 #pragma unroll
           for (int g = 0; g < NG; ++g) {
-            u32x4_t bw = src[kk][g];
-            if constexpr (CW) {
-              if (!((esmj >> (g * KU + kk)) & 1u) && !(a.diag & 128)) bw = wc_decode(bw, a.wc_eb2);
-            }
-            acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, as_bf16x8(bw), acc[g][mt], 0, 0, 0);
+            acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, as_bf16x8(src[kk][g]), acc[g][mt], 0, 0, 0);
           }
         }
       }
     };
-    // consume slot j, refill it.  CW: the slot is refilled FIRST (its coded words stay in
-    // other registers): the decode VALU work then runs with this stage's refill in flight
-    // instead of delaying it
+    // consume slot j, refill it
     auto step = [&](int j, int stage) {
-      if constexpr (CW) {
-        u32x4_t cur[KU][NG];
-#pragma unroll
-        for (int kk = 0; kk < KU; ++kk)
-#pragma unroll
-          for (int g = 0; g < NG; ++g) cur[kk][g] = wr[j][kk][g];
-        const uint32_t e = esm[j];
-        issue(wr[j], ar[j], mr[j], esm[j]);
-        consume(cur, ar[j], stage, e);
-      } else {
-        consume(wr[j], ar[j], stage, esm[j]);
-        issue(wr[j], ar[j], mr[j], esm[j]);
-      }
+      consume(wr[j], ar[j], stage);
+      issue(wr[j], ar[j]);
     };
     if (u + ustride < units) {  // the wave has a next unit: every refill exists
       for (int st = 0; st < S; st += R) {
@@ -721,7 +659,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         for (int j = 0; j < R; ++j) step(j, st + j);
       }
 #pragma unroll
-      for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j, esm[j]);
+      for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j);
     }
 
     if (a.diag & 2) {
@@ -862,7 +800,6 @@ inline constexpr Shape3 kShapes[] = {
     {8, 4, 4, 2, true},     // 4  (NG = 2)
     {8, 2, 4, 2, true},     // 5  gate/up (NG = 2)
     {16, 2, 8, 2, true},    // 6  (NG = 2)
-    {4, 16, 1, 2, false},   // 7  lm_head, 16-tile stages (TTS_HEAD_KU16=1)
 };
 inline constexpr int kNumShapes = sizeof(kShapes) / sizeof(kShapes[0]);
 inline bool shape_ng2(int c) { return kShapes[c].ng2; }
@@ -895,14 +832,7 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
   const dim3 g(grid, a.sliced ? a.kc : 1);
-  // the exponent-coded stream: one-row-tile launches of the matrices that have one (the
-  // epilogues built with it; the plain tiles stay for every other launch)
-  constexpr bool cw_built = EPI == EPI_LOGITS;
-  if (cw_built && mt == 1 && a.wc_rec && !a.sliced && !a.fattn_wgs) {
-    if (!a.wc_meta || !a.wc_esc) throw std::runtime_error("wgemm: incomplete coded weight stream");
-    hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY, cw_built>), g,
-                       dim3(WAVES * 64), lds, s, a);
-  } else if (mt == 1)
+  if (mt == 1)
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY>), g,
                        dim3(WAVES * 64), lds, s, a);
   else if (mt == 2)
@@ -951,7 +881,6 @@ static void launch_cfg(const WgemmArgs& a, int cfg, int grid, hipStream_t s) {
       case 1: launch_shape<1, NG, ASRC, NORM, EPI>(a, grid, s); break;
       case 2: launch_shape<2, NG, ASRC, NORM, EPI>(a, grid, s); break;
       case 3: launch_shape<3, NG, ASRC, NORM, EPI>(a, grid, s); break;
-      case 7: launch_shape<7, NG, ASRC, NORM, EPI>(a, grid, s); break;
       default: launch_shape<0, NG, ASRC, NORM, EPI>(a, grid, s); break;
     }
   }

@@ -107,14 +107,6 @@ struct WgemmArgs {
   int fattn_layer = 0;
   int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
-  // Exponent-coded weight stream (lm_wcomp.hip; one-row launches): the same tiles, lossless,
-  // 12 B per lane instead of 16 — per value its sign + 7 mantissa bits (a byte) and a 4-bit
-  // exponent code e - eb.  A tile with an exponent outside [eb, eb + 15] is kept raw in
-  // wc_esc (wc_meta[tile] = 1 + slot; 0 = coded).  Null: the plain bf16 tiles of `w`.
-  const uint32_t* wc_rec = nullptr;    // [tiles][64 lanes][3] u32
-  const uint32_t* wc_meta = nullptr;   // [tiles]
-  const bf16_t* wc_esc = nullptr;      // [escaped tiles][512] (the tile's own layout)
-  uint32_t wc_eb2 = 0;                 // (eb << 7) | (eb << 23)
 };
 
 struct WgemmPlan {
@@ -141,15 +133,6 @@ bool wgemm_supported(int M, int N, int K, int epi);
 bool wgemm_fattn_ok(int N, int K, int num_cu);
 bool wgemm_oproj_merge_ok(int M, int N, int K, int nsplit, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
-
-// ---- exponent-coded weight stream (lm_wcomp.hip): per 1 KiB tile the min / max bf16
-// exponent field over its 512 values, then the encode pass given eb and the escape slots
-void launch_wcomp_stats(const bf16_t* tiled, long long ntiles, uint8_t* emin, uint8_t* emax, hipStream_t s);
-void launch_wcomp_encode(const bf16_t* tiled, long long ntiles, uint32_t eb, const uint32_t* meta,
-                         uint32_t* rec, bf16_t* esc, hipStream_t s);
-// exact bf16 tiles back from the coded stream (tests: the round trip)
-void launch_wcomp_decode(const uint32_t* rec, const uint32_t* meta, const bf16_t* esc, uint32_t eb,
-                         long long ntiles, bf16_t* out, hipStream_t s);
 
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
 // MFMA blocks; epilogues EPI_STORE / EPI_RESID / EPI_SWIGLU; no fused RMSNorm
@@ -190,9 +173,6 @@ void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
 // decode step: register-streamed chunks of decode_split(D) positions, KV append fused
 int decode_split(int D);
 void launch_attn_decode_step(const AttnArgs& a, hipStream_t s);
-// decode step, one workgroup per (row, kv head): RoPE + KV append + attention + merge,
-// bf16 output in a.out [rows][H*D]
-void launch_attn_decode_merged(const AttnArgs& a, hipStream_t s);
 void launch_attn_combine(const AttnArgs& a, hipStream_t s);
 
 // ---- sampling head (lm_sample.hip): temperature, top-k, top-p, multinomial draw

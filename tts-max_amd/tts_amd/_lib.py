@@ -45,15 +45,12 @@ EXPORTED_SYMBOLS = (
     "tts_lm_score",
     "tts_lm_id_to_code",
     "tts_lm_last_timing",
-    "tts_lm_decode_path",
     "tts_lm_bench_kernel",
-    "tts_lm_coded_weights",
     "tts_codec_load",
     "tts_codec_decode",
     "tts_codec_samples_per_code",
     "tts_synth_fill",
     "tts_op_retile",
-    "tts_op_wcomp_roundtrip",
     "tts_op_wgemm",
     "tts_op_pgemm",
     "tts_op_sample",
@@ -170,15 +167,12 @@ def load_library() -> ctypes.CDLL:
         "tts_lm_score": (I32, [P, pi32, pi32, I32, I32, ctypes.POINTER(ctypes.c_float), P]),
         "tts_lm_id_to_code": (I32, [P, pi32, I32, pi32]),
         "tts_lm_last_timing": (I32, [P, ctypes.POINTER(F32), ctypes.POINTER(F32), pi32]),
-        "tts_lm_decode_path": (I32, [P, pi32]),
-        "tts_lm_coded_weights": (I32, [P, I32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), pi32]),
         "tts_lm_bench_kernel": (I32, [P, I32, I32, I32, I32, ctypes.POINTER(F32), ctypes.POINTER(ctypes.c_double)]),
         "tts_codec_load": (I32, [P, ctypes.POINTER(CodecConfig), ctypes.POINTER(TensorDesc), I32]),
         "tts_codec_decode": (I32, [P, pi32, pi32, I32, P, I32, ctypes.POINTER(ctypes.c_int64), P]),
         "tts_codec_samples_per_code": (I32, [P, pi32]),
         "tts_synth_fill": (I32, [P, I32, I64, U64, F32, P]),
         "tts_op_retile": (I32, [P, P, I32, I32, I32, P]),
-        "tts_op_wcomp_roundtrip": (I32, [P, I64, P, pi32, ctypes.POINTER(ctypes.c_int64), P]),
         "tts_op_wgemm": (I32, [P, I32, I32, I32, P, I32, P, F32, P, I32, P, I32, P]),
         "tts_op_pgemm": (I32, [P, I32, I32, P, I32, P, I32, P, I32, P]),
         "tts_op_sample": (I32, [P, I32, I32, F32, I32, F32, ctypes.c_uint64, I32, P, I32, P, P, P]),

@@ -233,6 +233,10 @@ class LLM:
         key = (temperature, stop[0] if stop else -1, int(getattr(sp, "min_tokens", 0) or 0),
                float(getattr(sp, "repetition_penalty", 1.0) or 1.0), top_k, float(getattr(sp, "top_p", 1.0) or 1.0),
                float(getattr(sp, "frequency_penalty", 0.0) or 0.0))
+        old = self._batchers.get(key)
+        if old is not None and old.error is not None:  # a batcher that died on an engine error:
+            old.close()                                 # replace it instead of failing every later call
+            del self._batchers[key]
         if key not in self._batchers:
             for b in self._batchers.values():  # one slot batch open per engine at a time
                 b._opened = False

@@ -242,7 +242,11 @@ class MI355XSpeechLM:
                         top_k: int | None = None, seed: int | None = None):
         """Chunked generation (config 5): yields (new_tokens_per_row, all_done) after the first
         token and then after every `chunk` further decode steps.  The rows' final tokens are
-        identical to generate_batch with the same arguments (same device loop, paused)."""
+        identical to generate_batch with the same arguments (same device loop, paused).
+
+        The engine lock is held while the generator is alive (one open generation per
+        engine): consume it to the end or close() it, in the thread that created it —
+        closing (or garbage collection) releases the lock through the `with` block."""
         if do_sample and seed is None:
             seed = int(torch.randint(0, 2**62, (1,)).item())
         B = len(prompts)
@@ -317,34 +321,18 @@ class MI355XSpeechLM:
                                           out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), None))
         return torch.from_numpy(out)
 
-    def decode_persistent(self) -> bool:
-        """True when the one-row decode step runs as the persistent launch (lm_persist.hip)."""
-        v = ctypes.c_int32(0)
-        if not hasattr(self._lib, "tts_lm_decode_path"):  # (an older build under A/B)
-            return False
-        _lib.check(self._lib.tts_lm_decode_path(self._h, ctypes.byref(v)))
-        return bool(v.value)
-
     def last_timing(self) -> tuple[float, float, int]:
         a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int32()
         _lib.check(self._lib.tts_lm_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value
-
-    def coded_weights(self, on: bool | None = None) -> dict:
-        """The lm_head's exponent-coded (lossless, 12-bit) weight stream: switch it on / off for
-        the one-row-tile launches (None: leave as is) and report its tiles / escaped tiles / eb."""
-        nt, ne, eb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
-        flag = -1 if on is None else int(bool(on))
-        _lib.check(self._lib.tts_lm_coded_weights(self._h, flag, ctypes.byref(nt), ctypes.byref(ne), ctypes.byref(eb)))
-        return {"tiles": nt.value, "escaped": ne.value, "eb": eb.value}
 
     KERNELS = ("qkv", "o_proj", "gate_up", "down", "lm_head", "attention")
 
     def bench_kernel(self, which: str, rows: int = 1, ctx: int = 450, iters: int = 50) -> tuple[float, float]:
         """(avg ms per launch, algorithmic bytes per launch) of one decode-step kernel."""
         ms, b = ctypes.c_float(), ctypes.c_double()
-        # qkv_attn: QKV + fused attention; persist: the whole one-row stack as one launch
-        sel = {"qkv_attn": 6, "persist": 7}.get(which)
+        # qkv_attn: QKV with the decode attention fused in (the one-row step's form)
+        sel = {"qkv_attn": 6}.get(which)
         sel = self.KERNELS.index(which) if sel is None else sel
         _lib.check(self._lib.tts_lm_bench_kernel(self._h, sel, rows, ctx, iters,
                                                  ctypes.byref(ms), ctypes.byref(b)))
