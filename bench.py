@@ -339,6 +339,25 @@ def synthetic_codes(lm, ids):
     return [c if c >= 0 else i % 65536 for i, c in zip(ids, lm.ids_to_codes(ids))]
 
 
+def _cpu_quota():
+    """CPUs this process may actually use: the cgroup CPU quota when one is set (the GPU box
+    gives a job a share of the host, while its affinity mask lists every host CPU)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def _cpu_info():
     model = "unknown"
     try:
@@ -373,33 +392,42 @@ def cpu_baseline(arch, carch, prompt, N, args):
     from tts_amd import configs, synth
 
     cpu_model, ncpu, avail = _cpu_info()
+    quota = _cpu_quota()
+    usable = min(avail, quota) if quota else avail
     t0 = time.time()
     model = hf_model(arch, synth.lm_weights_cpu(arch, 0x5EED))
-    log(f"cpu baseline: transformers model ready in {time.time() - t0:.1f}s ({cpu_model}, affinity {avail})")
+    log(f"cpu baseline: transformers model ready in {time.time() - t0:.1f}s ({cpu_model}, affinity {avail}, "
+        f"cgroup quota {quota})")
     ids = torch.tensor([prompt])
     eos = configs.vocab_for(arch).speech_end_id
     saved = torch.get_num_threads()
 
-    def lm_leg(threads, S):
+    def lm_leg(threads, S, max_time):
+        """(prefill s, s per generated code, codes generated); the generate call stops after
+        max_time seconds (HF MaxTimeCriteria), so an oversubscribed leg stays bounded."""
         torch.set_num_threads(threads)
         with torch.no_grad():
             model(ids[:, :16])  # thread-pool warm-up
             t1 = time.perf_counter()
             model(ids)  # prefill alone (its time is subtracted from the generate call below)
             t_prefill = time.perf_counter() - t1
+            log(f"cpu baseline: {threads} threads: prefill {t_prefill:.2f}s")
             t2 = time.perf_counter()
             out = model.generate(input_ids=ids, max_length=len(prompt) + S, min_new_tokens=S,
-                                 eos_token_id=eos, do_sample=False, repetition_penalty=1.1)
+                                 eos_token_id=eos, do_sample=False, repetition_penalty=1.1, max_time=max_time)
             t_gen = time.perf_counter() - t2
-        assert out.shape[1] == len(prompt) + S
-        return t_prefill, max(t_gen - t_prefill, 1e-9) / (S - 1)  # the first new token comes from the prefill
+        n = out.shape[1] - len(prompt)
+        assert n >= 2, "cpu baseline: the generate call produced fewer than 2 codes in its time budget"
+        return t_prefill, max(t_gen - t_prefill, 1e-9) / (n - 1), n  # the first new code comes from the prefill
 
     legs = {}
-    for threads in sorted({avail, 16}):
-        # the all-core leg may oversubscribe the box's CPU share: a shorter sample
-        S = args.cpu_steps if threads <= 16 else max(16, args.cpu_steps // 4)
-        legs[threads] = (S,) + lm_leg(threads, S)
-        log(f"cpu baseline: {threads} threads: prefill {legs[threads][1]:.2f}s, {legs[threads][2] * 1000:.1f} ms/code")
+    for threads in sorted({usable, 16}):
+        # (above the box's CPU share the leg oversubscribes it: a short, time-bounded sample)
+        S, budget = (args.cpu_steps, 60.0) if threads <= 16 else (max(16, args.cpu_steps // 4), 20.0)
+        log(f"cpu baseline: {threads} threads, prefill + up to {S} codes ({budget:.0f} s budget) ...")
+        t_p, t_d, n = lm_leg(threads, S, budget)
+        legs[threads] = (n, t_p, t_d)
+        log(f"cpu baseline: {threads} threads: {n} codes, {t_d * 1000:.1f} ms/code")
     best = min(legs, key=lambda t: legs[t][1] + (N - 1) * legs[t][2])
     del model
     torch.set_num_threads(best)
@@ -417,7 +445,8 @@ def cpu_baseline(arch, carch, prompt, N, args):
         "unit": "audio-codes/s",
         "cores": best,
         "kind": "reference",
-        "cpu": {"model": cpu_model, "nproc": ncpu, "affinity": avail},
+        "cpu": {"model": cpu_model, "nproc": ncpu, "affinity": avail, "cgroup_quota_cpus": quota,
+                "usable": usable},
         "by_threads": {str(t): {"codes_per_s": round(N / (v[1] + (N - 1) * v[2] + t_codec), 3),
                                 "prefill_s": round(v[1], 3), "ms_per_code": round(1000 * v[2], 2),
                                 "sample_codes": v[0]} for t, v in legs.items()},

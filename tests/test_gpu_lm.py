@@ -22,6 +22,9 @@ from oracle import lm_oracle
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# engine-vs-transformers bar of test_tts1_teacher_forced_logits_vs_transformers
+TF_MAX, TF_MEAN = 0.55, 0.1  # 1.25x the measured 0.4375 / 0.0793 (profiles/r3_tts1_tf_logit_dev.json)
 # absolute, on logits of magnitude ~1-20.  The oracle (torch CPU) and the GPU sum the fp32
 # dot products in different orders (split-K trees chosen per matrix by the stream plan), so
 # bf16 activations differ by an ulp here and there and the difference compounds over the
@@ -353,5 +356,14 @@ def test_tts1_teacher_forced_logits_vs_transformers():
                 assert int(idx[off + i][int(torch.argmax(got[i]))]) == int(idx[off + i][0]), i
         off += n
     d = torch.cat(devs)
-    assert d.max().item() <= 1.0, d.max().item()
-    assert d.mean().item() <= 0.16, d.mean().item()
+    # the measured deviation is recorded (gpurun_out/ on the box; committed under profiles/)
+    import json
+
+    rec = {"max_abs": d.max().item(), "mean_abs": d.mean().item(), "n": int(d.numel()),
+           "bar_max": TF_MAX, "bar_mean": TF_MEAN}
+    print("engine vs transformers teacher-forced logits:", rec)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "tts1_tf_logit_dev.json"), "w") as f:
+        json.dump(rec, f)
+    assert d.max().item() <= TF_MAX, d.max().item()
+    assert d.mean().item() <= TF_MEAN, d.mean().item()

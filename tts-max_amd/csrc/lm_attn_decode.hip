@@ -6,13 +6,12 @@
 // scale D^-0.5 and flash numerics (p = exp(s - max) in fp32, P rounded to bf16 for P.V,
 // fp32 normaliser; see oracle/lm_oracle.py).
 //
-// MI355X design.  One workgroup = one (sequence, kv head, chunk of SPLIT positions); its
-// four waves are the four q heads of the GQA group.  Every K/V byte of the chunk is loaded
-// at kernel entry (one HBM round trip), parked in padded LDS tiles, and the math runs
-// lane-per-position (scores) and lane-per-dimension (P.V) out of LDS, so there are no
-// cross-lane shuffles: the softmax statistics use DPP reductions (VALU speed) instead of
-// __shfl_xor, which lowers to ds_bpermute and serialises on LDS latency.  Chunks of one
-// sequence are merged later (o_proj prologue or attn_combine_kernel).
+// MI355X design.  One workgroup = one (sequence, kv head, chunk of SPLIT positions).  Every
+// K/V byte of the chunk is loaded at kernel entry by its four waves (one HBM round trip) and
+// parked in padded LDS tiles; then one wave computes the four q heads of the GQA group on
+// the matrix cores (lm_attn_chunk.h: S^T = K.Q^T, chunk softmax, O^T = V^T.P^T with the V
+// tile read transposed by ds_read_b64_tr_b16).  Chunks of one sequence are merged later
+// (o_proj prologue or attn_combine_kernel).
 #include "hip_common.h"
 #include "lm_kernels.h"
 #include "lm_attn_chunk.h"
@@ -34,7 +33,6 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[SPLIT * KROW];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[SPLIT * KROW];
   __shared__ __attribute__((aligned(16))) float qs[G * D];
-  __shared__ float ps[G * SPLIT];
 
   const int nrk = a.rows * a.KVH, nb = nrk * a.nsplit;
   if ((int)blockIdx.x >= nb) return;
@@ -93,13 +91,15 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
     Ks[(pos - t0) * KROW + dk] = kb;
     Vs[(pos - t0) * KROW + dk] = vx;
   }
-  // 3. registers -> LDS tiles
+  // 3. registers -> LDS tiles (rows past the chunk's end zeroed: their p is 0 and 0 * NaN
+  //    from stale LDS would poison P.V)
+  const u32x4_t z4 = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int i = 0; i < LOADS; ++i) {
     const int q = tid + i * 256, tl = q / CH, c = q % CH, t = t0 + tl;
-    if (t < t1 && t != pos) {
-      *(u32x4_t*)(Ks + tl * KROW + c * 8) = kr4[i];
-      *(u32x4_t*)(Vs + tl * KROW + c * 8) = vr4[i];
+    if (t != pos) {
+      *(u32x4_t*)(Ks + tl * KROW + c * 8) = t < t1 ? kr4[i] : z4;
+      *(u32x4_t*)(Vs + tl * KROW + c * 8) = t < t1 ? vr4[i] : z4;
     }
   }
   __syncthreads();
@@ -110,13 +110,12 @@ __global__ __launch_bounds__(256) void attn_decode2_kernel(AttnArgs a) {
     a.vcache[cbase + (size_t)pos * D + dk] = vx;
   }
 
-  // 4-6. scores (lane = position), chunk softmax statistics, P.V (lane = dimension)
-  const int g = wave;
-  float m, l;
-  attn_chunk_softmax<D, SPLIT>(Ks, qs + g * D, n, a.scale, lane, ps + g * SPLIT, m, l);
-  __syncthreads();
-  const size_t pidx = ((size_t)row * a.H + kvh * G + g) * a.nsplit + sp;
-  attn_chunk_pv_store<D, SPLIT>(Vs, ps + g * SPLIT, n, lane, m, l, a.part_o + pidx * D, a.part_ml + pidx * 2);
+  // 4-6. scores, chunk softmax statistics and P.V of the four q heads on the matrix cores
+  if (wave == 0) {
+    const size_t pidx = ((size_t)row * a.H + kvh * G) * a.nsplit + sp;
+    attn_chunk_mfma<D, SPLIT>(Ks, Vs, qs, n, a.scale, lane, a.part_o + pidx * D, a.part_ml + pidx * 2,
+                              a.nsplit * D, a.nsplit * 2);
+  }
 }
 
 int decode_split(int D) { return D == 64 ? 128 : 64; }

@@ -42,7 +42,7 @@ inline bool wgemm_attn_early(int M, int K, int nsplit, int waves) {
 // is this launch's, and the chunk math runs exactly as in attn_decode2 (lm_attn_chunk.h).
 constexpr int FATTN_D = 64, FATTN_SPLIT = 128, FATTN_G = 4;
 constexpr size_t fattn_lds_bytes() {
-  return (size_t)2 * FATTN_SPLIT * (FATTN_D + 8) * 2 + FATTN_G * FATTN_D * 4 + FATTN_G * FATTN_SPLIT * 4 +
+  return (size_t)2 * FATTN_SPLIT * (FATTN_D + 8) * 2 + FATTN_G * FATTN_D * 4 +
          (FATTN_G * FATTN_D / 2 + FATTN_D) * 4 + FATTN_D * 2;
 }
 constexpr int FATTN_MAX_SPINS = 1 << 16;  // ~0.1 s: the wait always ends (fattn_err set)
@@ -56,8 +56,7 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   bf16_t* Ks = (bf16_t*)smem;
   bf16_t* Vs = Ks + SPLIT * KROW;
   float* qs = (float*)(Vs + SPLIT * KROW);
-  float* ps = qs + G * D;
-  uint32_t* raw = (uint32_t*)(ps + G * SPLIT);  // q pairs [G*D/2] | k pairs [D/2] | v pairs [D/2]
+  uint32_t* raw = (uint32_t*)(qs + G * D);  // q pairs [G*D/2] | k pairs [D/2] | v pairs [D/2]
   const bf16_t* rawb = (const bf16_t*)raw;
   bf16_t* knew = (bf16_t*)(raw + G * D / 2 + D);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -88,14 +87,15 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   const int qi = min(tid, G * D - 1), qd = qi % D;
   const float qc = bf2f(a.rope_cos[(size_t)pos * D + qd]), qsn = bf2f(a.rope_sin[(size_t)pos * D + qd]);
 
-  auto stage_chunk = [&](int sp) {  // registers -> LDS tiles (the new position excluded)
-    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx);
+  auto stage_chunk = [&](int sp) {  // registers -> LDS tiles (the new position excluded;
+    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx);  // rows past the end zeroed)
+    const u32x4_t z4 = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < LOADS; ++i) {
       const int q = tid + i * NT, tl = q / CH, c = q % CH, t = t0 + tl;
-      if (q < SPLIT * CH && t < t1 && t != pos) {
-        *(u32x4_t*)(Ks + tl * KROW + c * 8) = kr4[i];
-        *(u32x4_t*)(Vs + tl * KROW + c * 8) = vr4[i];
+      if (q < SPLIT * CH && t != pos) {
+        *(u32x4_t*)(Ks + tl * KROW + c * 8) = t < t1 ? kr4[i] : z4;
+        *(u32x4_t*)(Vs + tl * KROW + c * 8) = t < t1 ? vr4[i] : z4;
       }
     }
   };
@@ -145,12 +145,10 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     }
     __syncthreads();  // tiles, qs visible
     if ((sp + nslot) * SPLIT < ctx) load_chunk(sp + nslot);  // next chunk in flight
-    if (wave < G) {
-      float m, l;
-      attn_chunk_softmax<D, SPLIT>(Ks, qs + wave * D, n, a.scale, lane, ps + wave * SPLIT, m, l);
-      const size_t pidx = ((size_t)row * a.H + kvh * G + wave) * a.nsplit + sp;
-      attn_chunk_pv_store<D, SPLIT>(Vs, ps + wave * SPLIT, n, lane, m, l, a.part_o + pidx * D,
-                                    a.part_ml + pidx * 2);
+    if (wave == 0) {  // the four q heads on the matrix cores (lm_attn_chunk.h)
+      const size_t pidx = ((size_t)row * a.H + kvh * G) * a.nsplit + sp;
+      attn_chunk_mfma<D, SPLIT>(Ks, Vs, qs, n, a.scale, lane, a.part_o + pidx * D, a.part_ml + pidx * 2,
+                                a.nsplit * D, a.nsplit * 2);
     }
   }
   // the new position's roped k and v to the cache, after the chunk math: a store issued
