@@ -80,9 +80,11 @@ struct LmWork {
   int cap_rows = 0;    // activation rows (prefill rows and decode batch)
   int cap_batch = 0;
   int cap_seq = 0;
-  DevBuf kv;           // [L][2][slots][KVH][max_seq][D]
+  DevBuf kv;           // per layer: K [slots][KVH][kv_stride][D], V^T [slots][KVH][D][kv_stride]
+  int kv_stride = 0;   // positions per (slot, kv head) strip: max_seq_len rounded up to 64
   DevBuf x, xn, qkv, attn_out, act, q_rot, last_x;  // activations
-  DevBuf part_o, part_ml;                           // attention split partials
+  DevBuf blocks;                                    // prefill query blocks (int4, lm_attn.hip)
+  int nblocks = 0;
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
@@ -95,8 +97,6 @@ struct LmWork {
   DevBuf seen;                                      // [B][V/32]
   DevBuf out_ids;                                   // [B][max_new]
   int out_cap = 0;
-  int nsplit_decode = 0, split_decode = 0;
-  int nsplit_prefill = 0, split_prefill = 0;
   hipGraphExec_t graph = nullptr;
   int graph_batch = -1;  // the captured step bakes in B, penalty, eos and min_new
   float graph_pen = -1.f;

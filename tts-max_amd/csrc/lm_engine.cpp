@@ -225,7 +225,9 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.cap_rows = R;
   w.cap_batch = B;
   w.cap_seq = S;
-  w.kv.alloc((size_t)L * 2 * B * KVH * S * D * 2);
+  w.kv_stride = (S + 63) / 64 * 64;  // (V^T fragments: 8 positions = 16 B, aligned)
+  w.kv.alloc((size_t)L * 2 * B * KVH * w.kv_stride * D * 2);
+  HIP_CHECK(hipMemsetAsync(w.kv.p, 0, w.kv.bytes, s));  // never-read garbage stays finite
   w.x.alloc((size_t)R * HID * 2);
   w.xn.alloc((size_t)R * HID * 2);
   w.qkv.alloc((size_t)R * QKV * 2);
@@ -233,14 +235,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.q_rot.alloc((size_t)R * H * D * 2);
   w.act.alloc((size_t)R * FF * 2);
   w.last_x.alloc((size_t)B * HID * 2);
-  w.split_decode = decode_split(D);
-  w.nsplit_decode = (S + w.split_decode - 1) / w.split_decode;
-  w.split_prefill = 512;  // = the kv block of torch's CPU flash kernel (kv_split_size)
-  w.nsplit_prefill = (S + w.split_prefill - 1) / w.split_prefill;
-  const size_t part_rows =
-      std::max((size_t)R * w.nsplit_prefill, (size_t)B * w.nsplit_decode);
-  w.part_o.alloc(part_rows * H * D * 4);
-  w.part_ml.alloc(part_rows * H * 2 * 4);
+  w.blocks.alloc(((size_t)R / 16 + B + 1) * 16);  // prefill query blocks: <= rows/16 + one per sequence
   w.gran.alloc((size_t)QKV / 2 * 8);
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
@@ -365,35 +360,33 @@ struct Ctx {
   AttnArgs attn_args(int layer, int rows, const int* slot, const int* pos, bool decode) {
     AttnArgs a;
     const int H = c.num_heads, KVH = c.num_kv_heads, D = c.head_dim;
-    const size_t kv_layer = (size_t)c.max_batch * KVH * c.max_seq_len * D;
+    const size_t kv_layer = (size_t)c.max_batch * KVH * w.kv_stride * D;
     a.qkv = w.qkv.as<bf16_t>(); a.ld_qkv = QKV(); a.rows = rows;
     a.row_slot = slot; a.row_pos = pos;
     a.kcache = w.kv.as<bf16_t>() + (size_t)layer * 2 * kv_layer;
-    a.vcache = a.kcache + kv_layer;
-    a.max_seq = c.max_seq_len;
+    a.vtcache = a.kcache + kv_layer;
+    a.max_seq = w.kv_stride;
     a.rope_cos = M.rope.as<bf16_t>();
     a.rope_sin = a.rope_cos + (size_t)c.max_seq_len * D;
     a.H = H; a.KVH = KVH; a.D = D;
     a.scale = (float)(1.0 / sqrt((double)D));
-    a.split = decode ? w.split_decode : w.split_prefill;
-    a.nsplit = decode ? w.nsplit_decode : w.nsplit_prefill;
-    a.part_o = w.part_o.as<float>(); a.part_ml = w.part_ml.as<float>();
     a.q_rot = w.q_rot.as<bf16_t>(); a.out = w.attn_out.as<bf16_t>();
+    a.blocks = w.blocks.as<int4>(); a.nblocks = w.nblocks;
     return a;
   }
 
-  // The one-row decode step's QKV launch carries the attention (TTS-1 geometry: head dim 64,
-  // decode chunks of 128 positions); consecutive fused launches differ in (pos, layer)
+  // The one-row decode step's QKV launch carries the attention (TTS-1 geometry: head dim 64);
+  // consecutive fused launches differ in (pos, layer)
   bool fused_attn_ok(int rows, bool decode) const {
     return decode && rows == 1 && use_fused_attn() && c.head_dim == 64 &&
-           w.split_decode == 128 && c.num_layers >= 2 && c.num_layers <= 64 &&
+           c.num_layers >= 2 && c.num_layers <= 64 &&
            wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
   }
   WgemmArgs fused_attn_args(const AttnArgs& a, int layer) {
     WgemmArgs fx;
     fx.gran = w.gran.as<uint64_t>();
     fx.fa = a;
-    fx.fattn_wgs = a.rows * a.KVH * std::min(8, a.nsplit);
+    fx.fattn_wgs = a.rows * a.KVH;
     fx.fattn_layer = layer;
     fx.fattn_err = w.ferr.as<int>();
     return fx;
@@ -415,28 +408,16 @@ struct Ctx {
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE);
       }
-      // decode: the chunked kernel whose partials the o_proj prologue merges
-      // (rows <= 16: the merge scratch + A rows fit LDS beside the split-K partials)
-      const bool fuse_combine = decode && rows <= 16 &&
-                                wgemm_oproj_merge_ok(rows, HID, HD, w.nsplit_decode, e->num_cu);
+      // attention output (bf16 rows of w.attn_out): inside the QKV launch (one-row step), one
+      // workgroup per (row, kv head) (decode), or per query block x kv head (prefill)
       if (fattn) {
-        // (attention ran inside the QKV launch)
       } else if (decode) {
         launch_attn_decode_step(a, s);
       } else {
         launch_rope_append(a, s);
-        launch_attn_decode(a, false, s);
+        launch_attn_prefill(a, s);
       }
-      if (fuse_combine) {
-        WgemmArgs exo;
-        exo.attn_o = a.part_o; exo.attn_ml = a.part_ml; exo.attn_pos = pos;
-        exo.attn_split = a.split; exo.attn_nsplit = a.nsplit; exo.attn_D = a.D;
-        gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, &exo);
-      } else {
-        launch_attn_combine(a, s);
-        gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID,
-             w.x.as<bf16_t>(), EPI_RESID);
-      }
+      gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
@@ -503,7 +484,7 @@ static void check_launch() { HIP_CHECK(hipGetLastError()); }
 // Prefill a group of sequences [b0, b0+nb): rows = sum of their prompt lengths.
 static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, int B, int slot_base,
                                std::vector<int>& last_rows, int& rows) {
-  std::vector<int> slot, pos, tok;
+  std::vector<int> slot, pos, tok, blk;
   rows = 0;
   last_rows.resize(B);
   for (int b = 0; b < B; ++b) {
@@ -512,10 +493,15 @@ static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, 
       pos.push_back(i);
       tok.push_back(ids[rows + i]);
     }
+    // attention query blocks: up to 16 consecutive rows of one sequence (lm_attn.hip)
+    for (int t0 = 0; t0 < lens[b]; t0 += 16)
+      blk.insert(blk.end(), {rows + t0, std::min(16, lens[b] - t0), slot_base + b, t0});
     rows += lens[b];
     last_rows[b] = rows - 1;
   }
   TTS_REQUIRE(rows <= X.w.cap_rows, "total prompt rows exceed the prefill workspace");
+  X.w.nblocks = (int)blk.size() / 4;
+  HIP_CHECK(hipMemcpyAsync(X.w.blocks.p, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, X.s));
   HIP_CHECK(hipMemcpyAsync(X.w.row_slot.p, slot.data(), rows * 4, hipMemcpyHostToDevice, X.s));
   HIP_CHECK(hipMemcpyAsync(X.w.row_pos.p, pos.data(), rows * 4, hipMemcpyHostToDevice, X.s));
   HIP_CHECK(hipMemcpyAsync(X.w.row_idx.p, tok.data(), rows * 4, hipMemcpyHostToDevice, X.s));
@@ -943,13 +929,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = 1.1f; ex.eos_mask = st.eos_mask;
   ex.part_val = e->w.lpart_v.as<float>(); ex.part_idx = e->w.lpart_i.as<int>();
   ex.part_stride = LOGITS_MAX_PARTS;
-  // attention chunk partials for the fused o_proj prologue
-  launch_attn_decode_step(aa, s);
-  const bool fuse_o = rows <= 16 &&
-                      wgemm_oproj_merge_ok(rows, HID, HD, e->w.nsplit_decode, e->num_cu);
-  WgemmArgs exo;
-  exo.attn_o = aa.part_o; exo.attn_ml = aa.part_ml; exo.attn_pos = e->w.row_pos.as<int>();
-  exo.attn_split = aa.split; exo.attn_nsplit = aa.nsplit; exo.attn_D = aa.D;
+  launch_attn_decode_step(aa, s);  // (a real attention row for o_proj)
   double b = 0;
   const double act_rw = 2.0 * rows;
   // launches rotate over the layers (as the decode step does), so a layer's weights are
@@ -966,15 +946,9 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr, EPI_STORE);
         b = 2.0 * QKV * HID + act_rw * (HID + QKV) + 2.0 * HID;
         break;
-      case 1:  // as in the decode step: attention chunks merged in the prologue when they fit
-        if (fuse_o) {
-          X.gemm(nullptr, rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID, &exo);
-          b = 2.0 * HID * HD + act_rw * 2 * HID +
-              (double)rows * c.num_heads * ((ctx + aa.split - 1) / aa.split) * (c.head_dim + 2) * 4;
-        } else {
-          X.gemm(e->w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID);
-          b = 2.0 * HID * HD + act_rw * (HD + 2 * HID);
-        }
+      case 1:
+        X.gemm(e->w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, e->w.x.as<bf16_t>(), EPI_RESID);
+        b = 2.0 * HID * HD + act_rw * (HD + 2 * HID);
         break;
       case 2:
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, e->w.act.as<bf16_t>(), FF, nullptr, EPI_SWIGLU);

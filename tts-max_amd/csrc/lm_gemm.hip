@@ -167,17 +167,10 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
 // the register-staged RMSNorm prologue (the EARLY instantiation, as launch_one decides).
 bool wgemm_fattn_ok(int N, int K, int num_cu) {
   const WgemmPlan p = plan_wgemm(1, N, K, EPI_STORE, num_cu);
-  if (!p.a_lds || p.sliced || K > 4096) return false;
+  if (!p.a_lds || p.sliced || K > 4096 || p.sp.waves != DEC_NW) return false;  // (16-wave workgroups)
   const int kch = K / 8, NT = p.sp.waves * 64;
   const int ea = p.sp.waves >= 16 ? 1 : (p.sp.waves >= 8 ? 2 : 4);  // wgemm_ea
   return kch % 64 == 0 && (kch + NT - 1) / NT <= ea;
-}
-
-// o_proj with the attention-chunk merge as its prologue (A_ATTN): only where the merge
-// takes the register-staged form; otherwise the merge kernel + a plain o_proj is faster.
-bool wgemm_oproj_merge_ok(int M, int N, int K, int nsplit, int num_cu) {
-  const WgemmPlan p = plan_wgemm(M, N, K, EPI_RESID, num_cu);
-  return p.a_lds && !p.sliced && wgemm_attn_early(M, K, nsplit, p.sp.waves);
 }
 
 bool wgemm_supported(int M, int N, int K, int epi) {

@@ -8,13 +8,12 @@
 
 #include "hip_common.h"
 #include "lm_kernels.h"
-#include "lm_attn_chunk.h"
+#include "lm_attn_core.h"
 
 namespace tts {
 
-// register budget of the early prologue: A chunks per thread / attention chunks per group
+// register budget of the early prologue: A chunks per thread
 constexpr int wgemm_ea(int waves) { return waves >= 16 ? 1 : (waves >= 8 ? 2 : 4); }
-constexpr int wgemm_cpg(int waves) { return waves >= 16 ? 2 : 4; }
 // floats of the kernel's scratch region `red`: split-K partials of the waves with kpart > 0,
 // the lm_head argmax exchange, the early RMSNorm segment sums (+64 slack)
 __host__ __device__ inline int wgemm_red_floats(int waves, int ksplit, int ng, int mt, int M, int Kl) {
@@ -26,84 +25,51 @@ __host__ __device__ inline int wgemm_red_floats(int waves, int ksplit, int ng, i
   r = r > Kl / 2 ? r : Kl / 2;  // RMSNorm weight (bf16) parked here during the LDS-DMA prologue
   return r + 64;
 }
-#define WGEMM_NSX 8
-inline bool wgemm_attn_early(int M, int K, int nsplit, int waves) {
-  const int aitems = M * (K / 8), NT = waves * 64;
-  if (aitems > NT || nsplit > WGEMM_NSX) return false;
-  const int groups = NT / aitems;
-  return (nsplit + groups - 1) / groups <= wgemm_cpg(waves);
-}
 
 // ------------------------------------------------- attention fused into the QKV launch -----
-// One appended workgroup = one (row, kv head, chunk slot c0); it attends chunks c0,
-// c0 + nslot, ... of SPLIT positions.  Its first chunk's K/V rows are loaded at entry, while
-// the projection workgroups still stream the QKV weights; then threads poll the granules of
-// the group's q (and, in the workgroup holding the new position, k and v) until their tag
-// is this launch's, and the chunk math runs exactly as in attn_decode2 (lm_attn_chunk.h).
-constexpr int FATTN_D = 64, FATTN_SPLIT = 128, FATTN_G = 4;
+// One appended workgroup per (row, kv head) of the one-row decode step: its 16 waves issue
+// their first-pass K / V^T fragment loads at entry, while the projection workgroups still
+// stream the QKV weights; then threads poll the granules of the group's q and of the new k,
+// v until their tag is this launch's, and the attention runs exactly as attn_decode_kernel's
+// (lm_attn_core.h dec_attend: same waves, same order, same bits), writing the group's four
+// heads of the bf16 attention row (fa.out) that o_proj then reads as a plain A row.
+constexpr int FATTN_D = 64;
 constexpr size_t fattn_lds_bytes() {
-  return (size_t)2 * FATTN_SPLIT * (FATTN_D + 8) * 2 + FATTN_G * FATTN_D * 4 +
-         (FATTN_G * FATTN_D / 2 + FATTN_D) * 4 + FATTN_D * 2;
+  return (size_t)DEC_G * FATTN_D * 4 + (DEC_G * FATTN_D / 2 + FATTN_D) * 4 + 2 * FATTN_D * 2 +
+         (size_t)dec_red_floats<FATTN_D, DEC_NW>() * 4;
 }
 constexpr int FATTN_MAX_SPINS = 1 << 16;  // ~0.1 s: the wait always ends (fattn_err set)
 
 template <int NT>
 TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
-  constexpr int D = FATTN_D, SPLIT = FATTN_SPLIT, G = FATTN_G;
-  constexpr int KROW = D + 8, CH = D / 8, H2 = D / 2;
-  constexpr int LOADS = (SPLIT * CH + NT - 1) / NT;
+  static_assert(NT == DEC_NW * 64, "the fused attention runs on 16-wave workgroups");
+  constexpr int D = FATTN_D, PW = dec_pw<D>(), G = DEC_G, H2 = D / 2;
+  using C = DecShape<D, PW>;
   const AttnArgs& a = wa.fa;
-  bf16_t* Ks = (bf16_t*)smem;
-  bf16_t* Vs = Ks + SPLIT * KROW;
-  float* qs = (float*)(Vs + SPLIT * KROW);
-  uint32_t* raw = (uint32_t*)(qs + G * D);  // q pairs [G*D/2] | k pairs [D/2] | v pairs [D/2]
+  float* qs = (float*)smem;                   // [G][D] roped q
+  uint32_t* raw = (uint32_t*)(qs + G * D);    // q pairs [G*D/2] | k pairs [D/2] | v pairs [D/2]
   const bf16_t* rawb = (const bf16_t*)raw;
   bf16_t* knew = (bf16_t*)(raw + G * D / 2 + D);
+  bf16_t* vnew = knew + D;
+  float* red = (float*)(vnew + D);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nrk = a.rows * a.KVH;
-  const int nslot = wa.fattn_wgs / nrk;
-  const int rk = b % nrk, c0 = b / nrk;
-  const int row = rk / a.KVH, kvh = rk % a.KVH;
+  const int row = b / a.KVH, kvh = b % a.KVH;
   const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
-  if (c0 * SPLIT >= ctx) return;  // (whole workgroup, before any barrier)
-  const bool has_new = ((pos / SPLIT) - c0) % nslot == 0;
-  const size_t cbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
-  const bf16_t* kc = a.kcache + cbase;
-  const bf16_t* vc = a.vcache + cbase;
-
-  u32x4_t kr4[LOADS], vr4[LOADS];
-  auto load_chunk = [&](int sp) {
-    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx);
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {  // unconditional (clamped row)
-      const int q = min(tid + i * NT, SPLIT * CH - 1), tl = q / CH, c = q % CH;
-      const int t = (t0 + tl < t1) ? t0 + tl : t0;
-      kr4[i] = *(const u32x4_t*)(kc + (size_t)t * D + c * 8);
-      vr4[i] = *(const u32x4_t*)(vc + (size_t)t * D + c * 8);
-    }
-  };
-  load_chunk(c0);
-  const int qi = min(tid, G * D - 1), qd = qi % D;
+  const size_t kvbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
+  const bf16_t* kc = a.kcache + kvbase;
+  const bf16_t* vtc = a.vtcache + kvbase;
+  u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
+  if (wave * PW < ctx) {
+    dec_load_k<D, PW>(kc, wave * PW, ctx, lane, kf);
+    dec_load_v<D, PW>(vtc, a.max_seq, wave * PW, lane, vf);
+  }
+  const int qd = tid % D;
   const float qc = bf2f(a.rope_cos[(size_t)pos * D + qd]), qsn = bf2f(a.rope_sin[(size_t)pos * D + qd]);
 
-  auto stage_chunk = [&](int sp) {  // registers -> LDS tiles (the new position excluded;
-    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx);  // rows past the end zeroed)
-    const u32x4_t z4 = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int q = tid + i * NT, tl = q / CH, c = q % CH, t = t0 + tl;
-      if (q < SPLIT * CH && t != pos) {
-        *(u32x4_t*)(Ks + tl * KROW + c * 8) = t < t1 ? kr4[i] : z4;
-        *(u32x4_t*)(Vs + tl * KROW + c * 8) = t < t1 ? vr4[i] : z4;
-      }
-    }
-  };
-  stage_chunk(c0);  // before the wait: only q-dependent work remains after it
-
-  // wait for the projection's granules of this kv group
+  // wait for the projection's granules of this kv group: q of its G heads, the new k and v
   const uint32_t tag = ((uint32_t)pos << 6) | (uint32_t)wa.fattn_layer;
-  const int nq = G * D / 2, ngr = has_new ? nq + D : nq;
+  const int nq = G * D / 2, ngr = nq + D;
   if (tid < ngr) {
     int col;
     if (tid < nq) col = kvh * G * D + 2 * tid;
@@ -123,39 +89,22 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     raw[tid] = (uint32_t)v;
   }
   __syncthreads();
-  // RoPE of the group's q heads and of the new position's k
+  // RoPE of the group's q heads and of the new k (HF apply_rotary_pos_emb in bf16)
   if (tid < G * D) {
     const int g = tid / D;
     qs[tid] = rope_elem(rawb[tid], rawb[g * D + (qd < H2 ? qd + H2 : qd - H2)], qd < H2, qc, qsn);
+  } else if (tid < G * D + D) {
+    const int d = tid - G * D;
+    knew[d] = f2bf(rope_elem(rawb[G * D + d], rawb[G * D + (d < H2 ? d + H2 : d - H2)], d < H2, qc, qsn));
+    vnew[d] = rawb[G * D + D + d];
   }
-  if (has_new && tid < D) {
-    const bf16_t kb = f2bf(rope_elem(rawb[G * D + tid], rawb[G * D + (tid < H2 ? tid + H2 : tid - H2)],
-                                     tid < H2, qc, qsn));
-    knew[tid] = kb;
-  }
-  for (int sp = c0; sp * SPLIT < ctx; sp += nslot) {
-    const int t0 = sp * SPLIT, t1 = min(t0 + SPLIT, ctx), n = t1 - t0;
-    if (sp != c0) {
-      __syncthreads();  // the previous chunk's readers are done
-      stage_chunk(sp);
-    }
-    if (pos >= t0 && pos < t1 && tid < D) {
-      Ks[(pos - t0) * KROW + tid] = knew[tid];
-      Vs[(pos - t0) * KROW + tid] = rawb[G * D + D + tid];
-    }
-    __syncthreads();  // tiles, qs visible
-    if ((sp + nslot) * SPLIT < ctx) load_chunk(sp + nslot);  // next chunk in flight
-    if (wave == 0) {  // the four q heads on the matrix cores (lm_attn_chunk.h)
-      const size_t pidx = ((size_t)row * a.H + kvh * G) * a.nsplit + sp;
-      attn_chunk_mfma<D, SPLIT>(Ks, Vs, qs, n, a.scale, lane, a.part_o + pidx * D, a.part_ml + pidx * 2,
-                                a.nsplit * D, a.nsplit * 2);
-    }
-  }
-  // the new position's roped k and v to the cache, after the chunk math: a store issued
-  // before the loop would be waited for by its barriers (__syncthreads drains vmcnt)
-  if (has_new && tid < D) {
-    a.kcache[cbase + (size_t)pos * D + tid] = knew[tid];
-    a.vcache[cbase + (size_t)pos * D + tid] = rawb[G * D + D + tid];
+  __syncthreads();
+  dec_attend<D, PW, DEC_NW>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
+                            a.out + (size_t)row * a.H * D + kvh * G * D);
+  // the new position's roped k and v to the cache, after this workgroup's reads
+  if (tid < D) {
+    a.kcache[kvbase + (size_t)pos * D + tid] = knew[tid];
+    a.vtcache[kvbase + (size_t)tid * a.max_seq + pos] = vnew[tid];
   }
 }
 
@@ -173,7 +122,7 @@ TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
 
-constexpr int A_GLOBAL = 0, A_LDS = 1, A_ATTN = 2;
+constexpr int A_GLOBAL = 0, A_LDS = 1;
 
 // MT_MAX: compile-time bound on 16-row m-tiles (1 for decode, 4 for up to 64 rows)
 template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R,
@@ -181,7 +130,7 @@ template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM
 __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
-  constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && NORM && EARLY;
+  constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && NORM && EARLY && WAVES == DEC_NW;
   if constexpr (FATT) {
     if (a.fattn_wgs && (int)blockIdx.x >= (int)gridDim.x - a.fattn_wgs) {
       fattn_consumer<NT>(a, smem, blockIdx.x - (gridDim.x - a.fattn_wgs));
@@ -213,7 +162,6 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   bf16_t* xs = (bf16_t*)smem;
   const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
   float* red = (float*)(smem + xs_bytes);  // split-K partials of waves kpart > 0, scratch
-  float* xtra = red + wgemm_red_floats(WAVES, KSPLIT, NG, MT_MAX, M, a.K);  // A_ATTN scratch
 
   // stage st of the wave's item of unit uu = NG*KU consecutive tiles from this tile index
   const int ur = a.ur;
@@ -266,37 +214,6 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         for (int p = wave; p < ppr; p += WAVES)
           __builtin_amdgcn_global_load_lds((gptr_t)(a.normw + p * 512 + lane * 8), (lptr_t)((bf16_t*)red + p * 512),
                                            16, 0, 0);
-      }
-    }
-  }
-  // (b) attention chunk partials for the o_proj prologue: thread = (row, 8 dims) item x
-  //     chunk group; every chunk statistic of the item's head, CPG chunk vectors
-  constexpr int NSX = WGEMM_NSX, CPG = wgemm_cpg(WAVES);
-  const int NS = a.attn_nsplit;
-  const int aitems = M * kch;
-  const int agroups = (ASRC == A_ATTN && aitems <= NT) ? NT / aitems : 0;
-  const int acpg = agroups ? (NS + agroups - 1) / agroups : CPG + 1;
-  constexpr bool early_o = EARLY && ASRC == A_ATTN;  // (host: wgemm_attn_early)
-  float2 mle[NSX], mlo[CPG];
-  float4 poe[CPG][2];
-  int pose = 0;
-  if constexpr (early_o) {
-    if (!(a.diag & 64)) {
-      const int it = tid % aitems, grp = min(tid / aitems, agroups - 1);
-      const int D = a.attn_D, H = a.K / D;
-      const int m = it / kch, hd = (it - m * kch) * 8;
-      const size_t mh = (size_t)m * H + hd / D;
-      const int d = hd % D;
-      pose = a.attn_pos[m];
-#pragma unroll
-      for (int s = 0; s < NSX; ++s) mle[s] = *(const float2*)(a.attn_ml + (mh * NS + min(s, NS - 1)) * 2);
-#pragma unroll
-      for (int i = 0; i < CPG; ++i) {
-        const int s = min(grp * acpg + i, NS - 1);
-        const float* po = a.attn_o + (mh * NS + s) * D + d;
-        poe[i][0] = *(const float4*)po;
-        poe[i][1] = *(const float4*)(po + 4);
-        mlo[i] = *(const float2*)(a.attn_ml + (mh * NS + s) * 2);
       }
     }
   }
@@ -495,96 +412,6 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           }
         }
       }
-    }
-    __syncthreads();
-   }
-  } else if constexpr (ASRC == A_ATTN) {
-   if constexpr (early_o) {
-    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
-    const int it = tid % aitems, grp = tid / aitems;
-    const int ns = (pose + a.attn_split) / a.attn_split;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int s = 0; s < NSX; ++s) if (s < ns) mx = fmaxf(mx, mle[s].x);
-    float l = 0.f;
-#pragma unroll
-    for (int s = 0; s < NSX; ++s) if (s < ns) l += mle[s].y * expf(mle[s].x - mx);
-    const float il = 1.0f / l;
-    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < CPG; ++i) {
-      const int s = grp * acpg + i;
-      if (i < acpg && s < ns) {
-        const float fs = expf(mlo[i].x - mx) * il;
-        o[0] += poe[i][0].x * fs; o[1] += poe[i][0].y * fs; o[2] += poe[i][0].z * fs; o[3] += poe[i][0].w * fs;
-        o[4] += poe[i][1].x * fs; o[5] += poe[i][1].y * fs; o[6] += poe[i][1].z * fs; o[7] += poe[i][1].w * fs;
-      }
-    }
-    const int m = it / kch, hd = (it - m * kch) * 8;
-    if (agroups > 1) {  // chunk groups of an item summed in fixed order through LDS
-      if (grp < agroups) {
-        float4* op = (float4*)xtra + (size_t)(grp * aitems + it) * 2;
-        op[0] = make_float4(o[0], o[1], o[2], o[3]);
-        op[1] = make_float4(o[4], o[5], o[6], o[7]);
-      }
-      __syncthreads();
-      if (grp == 0) {
-        for (int g = 1; g < agroups; ++g) {
-          const float4* op = (const float4*)xtra + (size_t)(g * aitems + it) * 2;
-          const float4 v0 = op[0], v1 = op[1];
-          o[0] += v0.x; o[1] += v0.y; o[2] += v0.z; o[3] += v0.w;
-          o[4] += v1.x; o[5] += v1.y; o[6] += v1.z; o[7] += v1.w;
-        }
-      }
-    }
-    if (grp == 0) {
-      u32x4_t pk;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
-      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
-    }
-    __syncthreads();
-   } else {
-    // o[m][h*D+d] = sum_s o_s f_s,  f_s = e^(m_s - M) / sum_s' l_s' e^(m_s' - M)
-    // phase 1: one thread per (row, head) turns the chunk statistics into factors (LDS);
-    // phase 2: every thread merges its (row, head, dim) elements with independent loads.
-    const int D = a.attn_D, H = a.K / D, NS = a.attn_nsplit;
-    float* fac = xtra;
-    for (int mh = threadIdx.x; mh < M * H; mh += NT) {
-      const int m = mh / H;
-      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
-      const float* ml = a.attn_ml + (size_t)mh * NS * 2;
-      float mx = -INFINITY;
-      for (int s = 0; s < ns; ++s) mx = fmaxf(mx, ml[2 * s]);
-      float l = 0.f;
-      for (int s = 0; s < ns; ++s) {
-        const float f = expf(ml[2 * s] - mx);
-        fac[mh * NS + s] = f;
-        l += ml[2 * s + 1] * f;
-      }
-      const float il = 1.0f / l;
-      for (int s = 0; s < ns; ++s) fac[mh * NS + s] *= il;
-    }
-    __syncthreads();
-    // 8 consecutive dims per thread: two float4 loads per chunk, one 16-B LDS store
-    for (int e = threadIdx.x; e < M * a.K / 8; e += NT) {
-      const int m = (e * 8) / a.K, hd = (e * 8) % a.K, mh = m * H + hd / D, d = hd % D;
-      const int ns = (a.attn_pos[m] + a.attn_split) / a.attn_split;
-      const float* po = a.attn_o + (size_t)mh * NS * D + d;
-      const float* f = fac + mh * NS;
-      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int s = 0; s < ns; ++s) {
-        const float4 v0 = *(const float4*)(po + (size_t)s * D);
-        const float4 v1 = *(const float4*)(po + (size_t)s * D + 4);
-        const float fs = f[s];
-        o[0] += v0.x * fs; o[1] += v0.y * fs; o[2] += v0.z * fs; o[3] += v0.w * fs;
-        o[4] += v1.x * fs; o[5] += v1.y * fs; o[6] += v1.z * fs; o[7] += v1.w * fs;
-      }
-      u32x4_t pk;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(o[2 * q], o[2 * q + 1]);
-      *(u32x4_t*)(xs + (size_t)m * ldxs + hd) = pk;
     }
     __syncthreads();
    }
@@ -807,12 +634,10 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   const int mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
   lds += (size_t)wgemm_red_floats(WAVES, KSPLIT, NG, mt, a.M, a.K) * sizeof(float);
-  if (ASRC == A_ATTN)  // chunk factors (fallback path) or chunk-group partials (early path)
-    lds += std::max((size_t)a.M * (a.K / a.attn_D) * a.attn_nsplit, (size_t)WAVES * 64 * 8) * sizeof(float);
-  if (a.fattn_wgs) {  // QKV + fused decode attention (one row, D 64, chunks of 128)
-    if (!(EPI == EPI_STORE && ASRC == A_LDS && NORM && a.M == 1 && a.fa.D == FATTN_D &&
-          a.fa.split == FATTN_SPLIT && a.gran && a.fattn_err && !a.sliced))
-      throw std::runtime_error("wgemm: fused attention needs the one-row QKV launch (D 64, split 128)");
+  if (a.fattn_wgs) {  // QKV + fused decode attention (one row, D 64, 16-wave workgroups)
+    if (!(EPI == EPI_STORE && ASRC == A_LDS && NORM && a.M == 1 && a.fa.D == FATTN_D && WAVES == DEC_NW &&
+          a.gran && a.fattn_err && !a.sliced))
+      throw std::runtime_error("wgemm: fused attention needs the one-row 16-wave QKV launch (D 64)");
     if (!EARLY) throw std::runtime_error("wgemm: fused attention needs the register-staged prologue");
     lds = std::max(lds, fattn_lds_bytes());
     grid += a.fattn_wgs;
@@ -849,7 +674,6 @@ static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
   if (a.M <= 16) {
     const int kch = a.K / 8, NT = WAVES * 64;
     if (ASRC == A_LDS) early = (kch % 64 == 0) && (a.M * kch + NT - 1) / NT <= wgemm_ea(WAVES);
-    if (ASRC == A_ATTN) early = wgemm_attn_early(a.M, a.K, a.attn_nsplit, WAVES);
   }
   if constexpr (ASRC == A_GLOBAL) launch_one_e<WAVES, KU, NG, KSPLIT, ASRC, NORM, EPI, R, false>(a, grid, s);
   else if (early) launch_one_e<WAVES, KU, NG, KSPLIT, ASRC, NORM, EPI, R, true>(a, grid, s);

@@ -4,9 +4,7 @@
 namespace tts {
 
 void launch_wgemm_resid(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipStream_t s) {
-  const bool attn = a.attn_o != nullptr;
-  if (attn) launch_cfg<1, A_ATTN, false, EPI_RESID>(a, p.cfg, p.grid, s);
-  else if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_RESID>(a, p.cfg, p.grid, s);
+  if (!p.a_lds) launch_cfg<1, A_GLOBAL, false, EPI_RESID>(a, p.cfg, p.grid, s);
   else launch_cfg<1, A_LDS, false, EPI_RESID>(a, p.cfg, p.grid, s);
 }
 

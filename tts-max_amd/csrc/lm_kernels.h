@@ -46,19 +46,17 @@ struct AttnArgs {
   int rows = 0;
   const int* row_slot = nullptr;  // KV slot (sequence) of each query row
   const int* row_pos = nullptr;   // absolute position of each query row
-  bf16_t* kcache = nullptr;       // this layer: [slots][KVH][max_seq][D]
-  bf16_t* vcache = nullptr;
-  int max_seq = 0;
+  bf16_t* kcache = nullptr;       // this layer's K rows: [slots][KVH][max_seq][D]
+  bf16_t* vtcache = nullptr;      // this layer's V columns: [slots][KVH][D][max_seq]
+  int max_seq = 0;                // position stride of the cache (a multiple of 64)
   const bf16_t* rope_cos = nullptr;  // [max_seq][D]
   const bf16_t* rope_sin = nullptr;
   int H = 0, KVH = 0, D = 0;
   float scale = 0.f;
-  int split = 0;      // positions per split-K chunk
-  int nsplit = 0;     // max chunks per row (grid.y)
-  float* part_o = nullptr;  // [rows][H][nsplit][D]
-  float* part_ml = nullptr; // [rows][H][nsplit][2] (running max, sum)
   bf16_t* q_rot = nullptr;  // prefill: roped q [rows][H*D]
-  bf16_t* out = nullptr;    // [rows][H*D] bf16
+  bf16_t* out = nullptr;    // [rows][H*D] bf16 attention output
+  const int4* blocks = nullptr;  // prefill: query blocks {first row, rows (<= 16), slot, first position}
+  int nblocks = 0;
 };
 
 struct WgemmArgs {
@@ -79,12 +77,6 @@ struct WgemmArgs {
   float* part_val = nullptr;      // [M][part_stride]
   int* part_idx = nullptr;
   int part_stride = 0;
-  // A operand = attention output combined from split-K chunk partials (o_proj prologue);
-  // K = num_heads * attn_D, chunk layout as AttnArgs::part_o / part_ml
-  const float* attn_o = nullptr;
-  const float* attn_ml = nullptr;
-  const int* attn_pos = nullptr;
-  int attn_split = 0, attn_nsplit = 0, attn_D = 0;
   float* logits_out = nullptr;  // EPI_LOGITS: also store the processed fp32 logits [M][ldl] (sampling)
   const uint16_t* counts = nullptr;  // EPI_LOGITS: new-token counts [M][seen_stride*32] (frequency penalty)
   float freq_penalty = 0.f;
@@ -97,12 +89,12 @@ struct WgemmArgs {
   bf16_t* norm_out = nullptr;         //   with next_norm (eps) into norm_out [M][ldo]
   // QKV launch with the decode attention fused in (decode, one row): the projection's
   // workgroups publish q/k/v as data-tagged 8-byte granules {bf16 pair, tag} with
-  // agent-scope stores; fattn_wgs extra workgroups (blockIdx.x >= the GEMM grid) each load
-  // one K/V chunk, wait for their q (and the new k/v) granules and write the chunk
-  // partials exactly as attn_decode2 does.  tag = (pos << 6) | layer differs between any
+  // agent-scope stores; fattn_wgs extra workgroups (blockIdx.x >= the GEMM grid), one per kv
+  // head, load their K / V^T fragments, wait for their q (and the new k/v) granules and
+  // attend exactly as attn_decode_kernel does.  tag = (pos << 6) | layer differs between any
   // two consecutive launches, so a granule left by the previous launch never matches.
   uint64_t* gran = nullptr;   // [M][ldo / 2]
-  AttnArgs fa;                // the attention of this layer (decode split, part_o / part_ml)
+  AttnArgs fa;                // the attention of this layer (its output row: fa.out)
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
   int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
@@ -131,7 +123,6 @@ inline size_t wgemm_part_elems(const WgemmPlan& p, int M, int ldo) {
 }
 bool wgemm_supported(int M, int N, int K, int epi);
 bool wgemm_fattn_ok(int N, int K, int num_cu);
-bool wgemm_oproj_merge_ok(int M, int N, int K, int nsplit, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
 
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
@@ -168,12 +159,11 @@ void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp
                                 const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s);
 
 // ---- attention (lm_attn.hip)
-void launch_rope_append(const AttnArgs& a, hipStream_t s);       // prefill: rope q,k; append k,v
-void launch_attn_decode(const AttnArgs& a, bool fused_append, hipStream_t s);
-// decode step: register-streamed chunks of decode_split(D) positions, KV append fused
-int decode_split(int D);
+void launch_rope_append(const AttnArgs& a, hipStream_t s);  // prefill: rope q, k; K rows, V columns
+void launch_attn_prefill(const AttnArgs& a, hipStream_t s);  // prefill: causal attention per query block
+// decode step: one workgroup per (row, kv head): RoPE, attention over pos + 1 positions,
+// bf16 output, KV append
 void launch_attn_decode_step(const AttnArgs& a, hipStream_t s);
-void launch_attn_combine(const AttnArgs& a, hipStream_t s);
 
 // ---- sampling head (lm_sample.hip): temperature, top-k, top-p, multinomial draw
 struct SampleArgs {
