@@ -1,0 +1,75 @@
+"""The persistent one-row decode step (lm_step.hip, opt-in TTS_STEP=1) against the per-layer
+launches: the same layer stack over the same row and KV cache (tts_lm_step_probe), and the
+same greedy codes.  The two paths sum fp32 in different orders, so they agree to bf16
+rounding per layer, and the stack's drift stays far inside the transformers logit bar."""
+import ctypes
+import dataclasses
+import os
+
+import numpy as np
+import pytest
+
+from tts_amd import _lib, configs, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(layers):
+    from tts_amd.speechlm import MI355XSpeechLM
+
+    old = os.environ.get("TTS_STEP")
+    os.environ["TTS_STEP"] = "1"
+    try:
+        arch = dataclasses.replace(configs.TTS1, num_layers=layers, name=f"tts1-{layers}l")
+        return MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=1, max_seq_len=1024)
+    finally:
+        if old is None:
+            del os.environ["TTS_STEP"]
+        else:
+            os.environ["TTS_STEP"] = old
+
+
+def _probe(m, token, pos, path):
+    a = m.arch
+    n = a.hidden_size + (a.num_heads + 2 * a.num_kv_heads) * a.head_dim + a.num_heads * a.head_dim
+    out = np.zeros(n, dtype=np.float32)
+    _lib.check(m._lib.tts_lm_step_probe(m._h, token, pos, path, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return out
+
+
+def test_step_one_layer_matches_launches():
+    m = _model(1)
+    if not m.step_available():
+        pytest.skip("the persistent step needs 256 CUs")
+    H = m.arch.hidden_size
+    for pos in (0, 1, 5, 40, 700):
+        a, b = _probe(m, 128300 + pos, pos, 0), _probe(m, 128300 + pos, pos, 1)
+        # q|k|v and the attention output bit-identical, the residual within one bf16 ulp
+        np.testing.assert_array_equal(a[H:], b[H:])
+        assert np.abs(a[:H] - b[:H]).max() <= 2.0 ** -7 * max(1.0, np.abs(a[:H]).max())
+
+
+def test_step_full_stack_close_to_launches():
+    m = _model(configs.TTS1.num_layers)
+    if not m.step_available():
+        pytest.skip("the persistent step needs 256 CUs")
+    H = m.arch.hidden_size
+    for pos in (0, 2, 40):
+        a, b = _probe(m, 128300 + pos, pos, 0), _probe(m, 128300 + pos, pos, 1)
+        d = np.abs(a[:H] - b[:H])
+        assert np.isfinite(b).all()
+        assert d.max() < 0.75 and d.mean() < 0.1, (d.max(), d.mean())
+
+
+def test_step_generate_matches_launches():
+    m = _model(configs.TTS1.num_layers)
+    if not m.step_available():
+        pytest.skip("the persistent step needs 256 CUs")
+    vocab = configs.vocab_for(m.arch)
+    p = synth.synthetic_prompt(vocab, 3, 39, 150)
+    kw = dict(max_length=len(p) + 48, min_new_tokens=48, eos_token_id=-1, repetition_penalty=1.1)
+    on = m.generate_batch([p], **kw)[0]
+    m.set_step(False)
+    off = m.generate_batch([p], **kw)[0]
+    m.set_step(True)
+    assert on == off

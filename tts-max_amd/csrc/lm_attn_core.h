@@ -186,14 +186,16 @@ constexpr int dec_red_floats() { return NW * DEC_G * 2 + NW * DEC_G * D; }
 // callers load them before anything else).  qs: roped q [4][D] fp32 (LDS, visible); knew /
 // vnew: the new position's roped k and v (LDS bf16, visible).  out: the group's four heads'
 // output, bf16 [4][D] (row of attn_out at the group's first head).
-template <int D, int PW, int NW>
-TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, float scale, const float* qs,
-                        const bf16_t* knew, const bf16_t* vnew, float* red,
-                        u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
-                        u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out) {
+// (general form: `wave` / `tid` = this wave's / thread's index among the NW attending waves,
+// `bar` = a barrier over exactly those waves; dec_attend below: the whole workgroup)
+template <int D, int PW, int NW, class Bar>
+TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, float scale, const float* qs,
+                          const bf16_t* knew, const bf16_t* vnew, float* red,
+                          u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
+                          u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out, int wave,
+                          int tid, Bar bar) {
   using C = DecShape<D, PW>;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
   const int c = lane & 15, g = lane >> 4;
   const int npass = (ctx + NW * PW - 1) / (NW * PW);
   float* mred = red;                 // [NW][4]
@@ -230,7 +232,7 @@ TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, flo
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   if (lane < DEC_G) mred[wave * DEC_G + lane] = mx;
-  __syncthreads();
+  bar();
   float M = -INFINITY;
 #pragma unroll
   for (int w = 0; w < NW; ++w) M = fmaxf(M, mred[w * DEC_G + (c & 3)]);
@@ -262,7 +264,7 @@ TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, flo
       *(float4*)(ored + (wave * DEC_G + c) * D + 16 * dt + 4 * g) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
     if (g == 0) lred[wave * DEC_G + c] = lsum;
   }
-  __syncthreads();
+  bar();
   for (int i = tid; i < DEC_G * D; i += NW * 64) {
     const int h = i / D, d = i - h * D;
     float O = 0.f, L = 0.f;
@@ -273,6 +275,15 @@ TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, flo
     }
     out[h * D + d] = f2bf(O / L);
   }
+}
+
+template <int D, int PW, int NW>
+TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, float scale, const float* qs,
+                        const bf16_t* knew, const bf16_t* vnew, float* red,
+                        u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
+                        u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out) {
+  dec_attend_w<D, PW, NW>(kc, vtc, S, ctx, scale, qs, knew, vnew, red, kf0, vf0, out,
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { __syncthreads(); });
 }
 
 // RoPE of one element (HF apply_rotary_pos_emb in bf16: x*cos + rotate_half(x)*sin, each
