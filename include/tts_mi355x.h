@@ -204,7 +204,7 @@ tts_status tts_lm_step_mode(tts_engine* e, int32_t mode, int32_t* available);
  * step (lm_step.hip; TTS-1 geometry), 0 = the per-layer launches.  x_out (host fp32
  * [hidden + qkv width + heads * head_dim]) = the residual stream after the last layer (before
  * the final RMSNorm), then the last layer's q|k|v (before RoPE) and attention output.
- * path 2 = the persistent step with its phase stamps: x_out (fp32 [layers][CUs][16]) = the
+ * path 2 (3: hand-offs not awaited, results meaningless) = the persistent step with its phase stamps: x_out (fp32 [layers][CUs][16]) = the
  * microseconds of each phase event since the first stamp (-1 = not stamped on that CU). */
 tts_status tts_lm_step_probe(tts_engine* e, int32_t token, int32_t pos, int32_t path, float* x_out);
 

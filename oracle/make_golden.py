@@ -140,6 +140,14 @@ CHAIN_CASES = {
         (2, 60, dict(new=120, min_new=120, rep=1.0), "single"),   # no penalty: lagged ids win
         (3, 700, dict(new=200, min_new=200, rep=1.4), "single"),  # CLI penalty
     ] + [(10 + r, 10 + 190 * r, dict(new=500, min_new=500, rep=1.1), "batch") for r in range(8)]),
+    # TTS-1-Max (configs[3]'s model: 4096 wide, 32 layers, untied lm_head, head dim 128) at
+    # full depth; the chain rows also go into the untied lm_head (synth.chain_overrides)
+    "lm_chain_max": ("tts1-max", 0x5EED, [
+        (0, 300, dict(new=200, min_new=200, rep=1.1), "single"),
+        (1, 200, dict(new=200, min_new=100, rep=1.1), "single"),  # EOS unit 340 -> stops with EOS
+        (2, 60, dict(new=120, min_new=120, rep=1.0), "single"),
+        (3, 700, dict(new=200, min_new=200, rep=1.4), "single"),
+    ] + [(10 + r, 10 + 190 * r, dict(new=200, min_new=200, rep=1.1), "batch") for r in range(8)]),
 }
 
 
@@ -151,7 +159,7 @@ def chain_fixture(name: str, manifest: dict) -> None:
     t0 = time.time()
     w = synth.lm_weights_cpu(arch, seed)
     synth.apply_chain(w, arch, spec)
-    model = hf_model(arch, w)
+    model = hf_model(arch, w)  # (the oracle below shares w's bf16 storage: 2 copies in all)
     orc = lm_oracle.LlamaOracle(arch, w, max_seq_len=4096)
     eos = vocab.speech_end_id
     rec = dict(prompt_ids=[], prompt_lens=[], hf_new=[], hf_new_lens=[], hf_margins=[], hf_top2=[], max_length=[],

@@ -1092,7 +1092,7 @@ void lm_step_mode(Engine* e, int mode, int* available) {
 // stack (tests/test_gpu_step.py).
 void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
-  TTS_REQUIRE(path >= 0 && path <= 2, "bad probe path");
+  TTS_REQUIRE(path >= 0 && path <= 3, "bad probe path");
   TTS_REQUIRE(path == 0 || e->w.step_ok, "the persistent step is not available for this model");
   TTS_REQUIRE(pos >= 0 && pos < e->lm.cfg.max_seq_len && token >= 0 && token < e->lm.cfg.vocab_size, "bad probe");
   hipStream_t s = e->stream;
@@ -1103,13 +1103,15 @@ void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
   HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, &zero, 4, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(e->w.row_pos.p, &pos, 4, hipMemcpyHostToDevice, s));
   launch_embed(e->w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), 1, HID, s);
-  if (path == 2) {  // the persistent step with its per-phase stamps: x_out = [layer][CU][kStepEvents] us
+  if (path >= 2) {  // the persistent step with its per-phase stamps: x_out = [layer][CU][kStepEvents] us
+                    // (path 3: every hand-off taken as ready, results garbage: the stream's own pace)
     const size_t n = (size_t)X.c.num_layers * e->num_cu * kStepEvents;
     unsigned long long* tr = nullptr;
     HIP_CHECK(hipMalloc(&tr, n * 8));
     HIP_CHECK(hipMemsetAsync(tr, 0, n * 8, s));
     StepArgs sa = X.step_args(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
     sa.trace = tr;
+    sa.nodeps = path == 3;
     launch_decode_step(sa, s);
     HIP_CHECK(hipGetLastError());
     std::vector<unsigned long long> t(n);

@@ -147,6 +147,8 @@ struct StepArgs {
   int* done = nullptr;                          // arrival counter (0 between steps)
   int* err = nullptr;                           // set on a hand-off timeout
   unsigned long long* trace = nullptr;          // diagnostics: [layer][CU][kStepEvents] s_memrealtime stamps
+  int nodeps = 0;                               // diagnostics: take every hand-off as ready (wrong
+                                                //   results; the weight stream's own pace)
 };
 constexpr int kStepEvents = 16;
 bool step_supported(int hidden, int heads, int kv_heads, int head_dim, int ffn, int layers, int num_cu);

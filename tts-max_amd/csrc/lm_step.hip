@@ -6,14 +6,14 @@
 // Why one launch: as a chain of dependent launches a batch-1 layer pays, per launch, the
 // ramp of a fresh weight stream after its inputs are ready (MI355X_MICROARCH.md, price list
 // rows launches-baseline / engine-vs-launches / prefetch-credit).  Here every CU runs one
-// 16-wave workgroup for all layers:
+// 8-wave workgroup for all layers:
 //   * wave 0 is the LOADER: it streams this CU's share of every weight matrix, in the order
 //     the step consumes them (qkv, o, gate/up, down of layer 0, then layer 1, ...), through
 //     an LDS ring of 16 KiB slots by LDS-DMA (global_load_lds nt), FLY slots in flight, and
 //     never waits for a data dependency — only for a free slot.  While the CU waits for a
 //     vector from the other CUs, its ring keeps filling with the weights it will multiply
 //     next.
-//   * waves 1..15 are CONSUMERS: slot s of the step goes to consumer s % 15; a slot is a
+//   * waves 1..7 are CONSUMERS: slot s of the step goes to consumer s % 7; a slot is a
 //     self-contained piece of work (4 whole rows of a K = 2048 matrix, or 256 outputs of
 //     the CU's K-slice of the down projection), multiplied on the VALU (v_dot2_f32_bf16)
 //     against the op's input vector in LDS once it is there.
@@ -24,7 +24,7 @@
 // Vectors move between CUs as 8-byte granules {payload, tag} written by ONE agent-scope
 // store each (tag = the step's sequence number: a granule left by an earlier step never
 // matches) and gathered by one wave per vector per CU (MI355X_MICROARCH.md: granule,
-// allgather).  Attention runs on CUs 0..7 (one per kv head): their 15 consumer waves hold
+// allgather).  Attention runs on CUs 0..7 (one per kv head): their 7 consumer waves hold
 // the kv head's K rows / V^T columns in registers from the start of the layer
 // (lm_attn_core.h), gather q / k / v, and publish the head group's bf16 output.
 //
@@ -44,7 +44,7 @@ namespace tts {
 
 namespace {
 
-constexpr int NCU = 256, NWV = 16, NCONS = NWV - 1;
+constexpr int NCU = 256, NWV = 8, NCONS = NWV - 1;
 constexpr int HID = 2048, QKVN = 3072, FFN = 8192, NH = 32, NKV = 8, HDIM = 64, GQ = NH / NKV;
 constexpr int SLOT = 16384;                    // bytes per ring slot
 constexpr int NS = 8;                          // ring slots
@@ -81,7 +81,7 @@ constexpr int L_AO = L_KN + 2 * HDIM * 2;     // attention output of the group (
 constexpr int L_RED = L_AO + GQ * HDIM * 2;   // attention merge scratch
 constexpr int L_FLAGS = L_RED + dec_red_floats<HDIM, NCONS>() * 4;
 constexpr int F_FULL = 0, F_FREE = NS, F_RX = 2 * NS, F_RA = F_RX + 1, F_RH = F_RX + 2, F_ACT = F_RX + 3,
-              F_BAR = F_RX + 4, F_RED = F_RX + 5, F_N = F_RX + 8;
+              F_BAR = F_RX + 4, F_RED = F_RX + 5, F_DD = F_RX + 6, F_N = F_RX + 8;
 constexpr int LDS_BYTES = L_FLAGS + F_N * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "decode step LDS");
 
@@ -119,8 +119,9 @@ TTS_DEV void lds_wait_ge(lint* p, int v, int* err) {
 }
 
 // one granule's payload once its tag is this step's (bounded)
-TTS_DEV uint32_t gwait(const uint64_t* p, uint32_t tag, int* err) {
+TTS_DEV uint32_t gwait(const uint64_t* p, uint32_t tag, int* err, bool any = false) {
   uint64_t v = gld(p);
+  if (any) return (uint32_t)v;
   int spins = 0;
   while ((uint32_t)(v >> 32) != tag) {
     if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(err))) {
@@ -133,18 +134,36 @@ TTS_DEV uint32_t gwait(const uint64_t* p, uint32_t tag, int* err) {
   return (uint32_t)v;
 }
 
-// One wave gathers a bf16 vector of HID values (HID/2 granules, 16 per lane, all issued
-// before the first tag test) into LDS.
-TTS_DEV void gather_vec(const uint64_t* g, uint32_t tag, bf16_t* dst, int lane, int* err) {
+// One wave gathers a bf16 vector of HID values (HID/2 granules, 16 per lane) into LDS: one
+// sweep issues every load, then only the granules still stale are re-read, all of them per
+// re-sweep (never one round trip per granule).
+TTS_DEV void gather_vec(const uint64_t* g, uint32_t tag, bf16_t* dst, int lane, int* err, bool any) {
   constexpr int PER = HID / 2 / 64;
   uint64_t v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) v[i] = gld(g + lane + 64 * i);
+  uint32_t pending = 0;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    uint32_t w = (uint32_t)v[i];
-    if ((uint32_t)(v[i] >> 32) != tag) w = gwait(g + lane + 64 * i, tag, err);
-    ((uint32_t*)dst)[lane + 64 * i] = w;
+    if (any || (uint32_t)(v[i] >> 32) == tag) ((uint32_t*)dst)[lane + 64 * i] = (uint32_t)v[i];
+    else pending |= 1u << i;
+  }
+  int spins = 0;
+  while (pending) {
+    if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(err))) {
+      set_err(err);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (pending & (1u << i)) v[i] = gld(g + lane + 64 * i);
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if ((pending & (1u << i)) && (uint32_t)(v[i] >> 32) == tag) {
+        ((uint32_t*)dst)[lane + 64 * i] = (uint32_t)v[i];
+        pending &= ~(1u << i);
+      }
   }
 }
 
@@ -187,16 +206,21 @@ TTS_DEV void plain_chunks(const bf16_t* v, int lane, u32x4_t (&xn)[4]) {
 
 // the 4 rows of a K = 2048 slot against the lane's chunks: wave-uniform fp32 results
 TTS_DEV void rows4(const char* slot, const u32x4_t (&xn)[4], int lane, float (&y)[4]) {
+  u32x4_t w[4][4];  // all 16 LDS reads in flight before the first product
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[r][j] = *(const u32x4_t*)(slot + r * 4096 + j * 1024 + lane * 16);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc = dot8(*(const u32x4_t*)(slot + r * 4096 + j * 1024 + lane * 16), xn[j], acc);
+    for (int j = 0; j < 4; ++j) acc = dot8(w[r][j], xn[j], acc);
     y[r] = wave_sum_dpp(acc);
   }
 }
 
-// Attention of kv head c (CUs 0..7) by the 15 consumer waves: q of heads 4c..4c+3 and the
+// Attention of kv head c (CUs 0..7) by the 7 consumer waves: q of heads 4c..4c+3 and the
 // new k, v gathered from the qkv granules -> RoPE -> lm_attn_core.h dec_attend_w (global max,
 // bf16 P.V, wave-order merge) -> the group's 4 heads published; the new K row / V^T column to
 // the cache.
@@ -204,7 +228,7 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
                                                          int c, int cw, int ctid, int lane, int l, int pos, int ctx,
                                                          size_t kvl, size_t kvbase, int& nbar) {
   lint* fl = lflags(smem);
-  auto cbar = [&]() {  // barrier over the 15 consumer waves (LDS counter)
+  auto cbar = [&]() {  // barrier over the consumer waves (LDS counter)
     ++nbar;
     if (lane == 0) lds_add(fl + F_BAR, 1);
     lds_wait_ge(fl + F_BAR, NCONS * nbar, a.err);
@@ -230,9 +254,10 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
     if (ctid < NQ) col = c * GQ * HDIM + 2 * ctid;
     else if (ctid < NQ + HDIM / 2) col = NH * HDIM + c * HDIM + 2 * (ctid - NQ);
     else col = NH * HDIM + NKV * HDIM + c * HDIM + 2 * (ctid - NQ - HDIM / 2);
-    raw[ctid] = gwait(G + G_QKV + col / 2, tag, a.err);
+    raw[ctid] = gwait(G + G_QKV + col / 2, tag, a.err, a.nodeps);
   }
   cbar();
+  if (cw == 0 && lane == 0) stamp(a.trace, l, c, 14);
   const int qd = ctid % HDIM;
   const float qc = bf2f(a.rope_cos[(size_t)pos * HDIM + qd]), qsn = bf2f(a.rope_sin[(size_t)pos * HDIM + qd]);
   constexpr int H2 = HDIM / 2;
@@ -248,6 +273,7 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
   dec_attend_w<HDIM, PW, NCONS>(kc, vtc, a.kv_stride, ctx, a.scale, qs, knew, vnew, (float*)(smem + L_RED), kf, vf,
                                 ao, cw, ctid, cbar);
   cbar();
+  if (cw == 0 && lane == 0) stamp(a.trace, l, c, 15);
   if (ctid < GQ * HDIM / 2) gst(G + G_ATT + c * GQ * HDIM / 2 + ctid, ((const uint32_t*)ao)[ctid], tag);
   if (ctid < HDIM) {  // the new position into the cache (no other CU reads this (slot, kv head))
     bf16_t* kw = a.kv + 2 * kvl + kvbase;
@@ -261,26 +287,35 @@ __attribute__((noinline)) __device__ void step_loader(const void* stream, char* 
                                                       int* err, unsigned long long* tr) {
   lint* fl = lflags(smem);
   const char* src = (const char*)stream + (size_t)c * total * SLOT;
-  int pub = 0;  // first slot not yet published
+  int pub = 0;  // first slot not yet published (slots pub .. s-1 are in flight)
+  int spins = 0;
+  bool bad = false;
 #pragma unroll 1
   for (int s = 0; s < total; ++s) {
     const int r = s % NS;
     if (tr && lane == 0 && s % S_LAYER == 0) stamp(tr, s / S_LAYER, c, 12);
-    if (lds_ld(fl + F_FREE + r) != s - NS) {
-      // ring full: publish what is in flight, then wait for the slot
-      if (tr && lane == 0) stamp(tr, s / S_LAYER, c, 13);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (; pub < s; ++pub) lds_st(fl + F_FULL + pub % NS, pub);
-      int spins = 0;
-      while (lds_ld(fl + F_FREE + r) != s - NS) {
-        if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(err))) {
-          set_err(err);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    // ring full: while the slot is still being read, publish the in-flight slots as they land
+    // (oldest first, the newer ones stay in flight)
+    while (lds_ld(fl + F_FREE + r) != s - NS) {
+      const int inflight = s - pub;
+      if (inflight > 0) {
+        if (inflight >= 3) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else if (inflight == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_st(fl + F_FULL + pub % NS, pub);
+        ++pub;
+        continue;
       }
-      if (gerr(err)) break;
+      if (tr && lane == 0) stamp(tr, s / S_LAYER, c, 13);
+      if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(err))) {
+        set_err(err);
+        bad = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
+    if (bad) break;
+    spins = 0;
     const char* gs = src + (size_t)s * SLOT + lane * 16;
     char* ls = smem + L_RING + r * SLOT;
 #pragma unroll
@@ -330,7 +365,7 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
   do {                                         \
     if (tr && lane == 0) stamp(tr, l, c, (e)); \
   } while (0)
-  auto cbar = [&]() {  // barrier over the 15 consumer waves (LDS counter)
+  auto cbar = [&]() {  // barrier over the consumer waves (LDS counter)
     ++nbar;
     if (lane == 0) lds_add(fl + F_BAR, 1);
     lds_wait_ge(fl + F_BAR, NCONS * nbar, a.err);
@@ -347,7 +382,7 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
 #pragma unroll 1
   for (int l = 0; l < L; ++l) {
     // lane-derived addresses are recomputed per layer instead of being hoisted out of the
-    // loop (live across it they would not fit the 128 registers of a 16-wave workgroup)
+    // loop (live across it they would crowd the registers the attention and slot math need)
     int lane = tid & 63, ctid = tid - 64;
     asm volatile("" : "+v"(lane), "+v"(ctid));
     uint64_t* G = a.gran + (size_t)l * G_LAYER;
@@ -364,7 +399,10 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
 #pragma unroll
         for (int i = 0; i < HID / 512; ++i) *(u32x4_t*)(xs + 8 * lane + 512 * i) = *(const u32x4_t*)(a.x + 8 * lane + 512 * i);
       } else {
-        gather_vec(Gprev + G_X, tag, xs, lane, a.err);
+        // sweep once this CU's own part of x_l is out: by then the other CUs' parts are
+        // close, and the sweep's loads no longer queue beside this CU's down stream
+        lds_wait_ge(fl + F_RED, 4 * l, a.err);
+        gather_vec(Gprev + G_X, tag, xs, lane, a.err, a.nodeps);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) lds_st(fl + F_RX, l + 1);
@@ -396,7 +434,7 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
     }
     // 4. the attention output of all heads
     if (cw == 1) {
-      gather_vec(G + G_ATT, tag, as, lane, a.err);
+      gather_vec(G + G_ATT, tag, as, lane, a.err, a.nodeps);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) lds_st(fl + F_RA, l + 1);
       EV(4);
@@ -425,7 +463,7 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
     }
     // 6. h of all columns
     if (cw == 2) {
-      gather_vec(G + G_H, tag, hs, lane, a.err);
+      gather_vec(G + G_H, tag, hs, lane, a.err, a.nodeps);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) lds_st(fl + F_RH, l + 1);
       EV(6);
@@ -470,37 +508,66 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
           have = true;
         }
         on_slot(s, [&](const char* sl) {
+          u32x4_t w[4][4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[q][i] = *(const u32x4_t*)(sl + i * 4096 + (lane + 64 * q) * 16);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int nn = lane + 64 * q;  // slot layout [i][256 n][8]
             float acc = 0.f;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc = dot8(*(const u32x4_t*)(sl + i * 4096 + nn * 16), av[i], acc);
+            for (int i = 0; i < 4; ++i) acc = dot8(w[q][i], av[i], acc);
             const int n = 256 * t + nn;
             gst(G + G_PD + ((size_t)(n >> 3) * NCU + c) * 8 + (n & 7), __float_as_uint(acc), tag);
           }
         });
+        if (lane == 0) lds_add(fl + F_DD, 1);
         if (t == S_D - 1) EV(9);
       }
     }
     // 9. column owner: outputs 8c .. 8c+7 = sum over the 256 producers (fixed order), rounded,
     //    added to h -> x_{l+1} published (and, after the last layer, written for the lm_head)
-    if (cw >= 7) {
-      const int j = cw - 7;  // column 8c + j
-      const uint64_t* pd = G + G_PD + (size_t)c * NCU * 8 + j;
-      float v[4];
+    if (cw >= NCONS - 4) {
+      const int j0 = 2 * (cw - (NCONS - 4));  // columns 8c + j0, 8c + j0 + 1
+      // the 2 x 4 partials of this lane's producers 4 lane .. 4 lane + 3, re-swept together,
+      // first swept once this CU's own down slots are done (polling earlier would slow this
+      // CU's own weight stream for the slots still to come)
+      lds_wait_ge(fl + F_DD, S_D * (l + 1), a.err);
+      const uint64_t* pd = G + G_PD + (size_t)c * NCU * 8 + j0 + lane * 32;
+      float v[2][4];
+      uint64_t gv[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint64_t g = gld(pd + (4 * lane + i) * 8);
-        v[i] = __uint_as_float((uint32_t)(g >> 32) == tag ? (uint32_t)g : gwait(pd + (4 * lane + i) * 8, tag, a.err));
+      for (int k = 0; k < 8; ++k) gv[k] = gld(pd + (k & 3) * 8 + (k >> 2));
+      uint32_t pending = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pending |= ((uint32_t)(gv[k] >> 32) != tag && !a.nodeps) ? 1u << k : 0u;
+      int spins = 0;
+      while (pending) {
+        if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(a.err))) {
+          set_err(a.err);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (pending & (1u << k)) gv[k] = gld(pd + (k & 3) * 8 + (k >> 2));
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((uint32_t)(gv[k] >> 32) == tag) pending &= ~(1u << k);
       }
-      const float d = wave_sum_dpp((v[0] + v[1]) + (v[2] + v[3]));
-      if (j == 0) EV(10);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k >> 2][k & 3] = __uint_as_float((uint32_t)gv[k]);
+      const float d0 = wave_sum_dpp((v[0][0] + v[0][1]) + (v[0][2] + v[0][3]));
+      const float d1 = wave_sum_dpp((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
+      if (j0 == 0) EV(10);
       float* red = (float*)(smem + L_RED);  // (attention scratch: free by now)
       if (lane == 0) {
-        red[j] = rbf(bf2f(hs[8 * c + j]) + rbf(d));
+        red[j0] = rbf(bf2f(hs[8 * c + j0]) + rbf(d0));
+        red[j0 + 1] = rbf(bf2f(hs[8 * c + j0 + 1]) + rbf(d1));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lds_add(fl + F_RED, 1) == 8 * (l + 1) - 1) {  // the last column of this CU publishes
+        if (lds_add(fl + F_RED, 1) == 4 * (l + 1) - 1) {  // the last of the 4 publishes
           EV(11);
           for (int k = 0; k < 4; ++k) {
             const float x0 = red[2 * k], x1 = red[2 * k + 1];

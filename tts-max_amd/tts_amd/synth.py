@@ -124,7 +124,8 @@ def lm_weights_device(arch: configs.LmArch, seed: int, device) -> dict[str, torc
 # min-new-tokens EOS mask, EOS stop):
 #
 # * chain tokens c_0..c_{U-1} (distinct <|s_N|> ids) and EOS get embedding rows s*H_r, r a
-#   Sylvester-Hadamard row (exactly orthogonal, exact in bf16; tied => also their lm_head rows);
+#   Sylvester-Hadamard row (exactly orthogonal, exact in bf16), and so do their lm_head rows
+#   (the same tensor when tied, written separately when not);
 # * MLP unit j of layer 0 detects c_j (gate = up = 2^g H_{r(j)}) and writes
 #   2^q (H_{r(j+1)} + w_seen H_{r(j-lag)}) into the residual: the already-generated
 #   c_{j-lag} has the larger raw logit (x w_seen = 1.046875) but, penalised by
@@ -171,8 +172,8 @@ def chain_overrides(arch: configs.LmArch, spec: ChainSpec) -> dict[str, tuple[np
     """{tensor name: (index, rows)} — rows (float32, bf16-exact) that replace tensor[index]
     (rows of the embedding / gate / up; columns of down, given transposed)."""
     if arch.hidden_size & (arch.hidden_size - 1) or spec.units + 1 > arch.hidden_size or \
-            spec.units > arch.intermediate_size or not arch.tie_word_embeddings:
-        raise ValueError("chain model needs a tied, power-of-two hidden size >= units + 1")
+            spec.units > arch.intermediate_size:
+        raise ValueError("chain model needs a power-of-two hidden size >= units + 1")
     d = arch.hidden_size
     vocab = configs.vocab_for(arch)
     toks = chain_tokens(vocab, spec)
@@ -194,12 +195,15 @@ def chain_overrides(arch: configs.LmArch, spec: ChainSpec) -> dict[str, tuple[np
             down[j] = q * H[j + 1]
     p = "model.layers.0."
     unit_idx = np.arange(U, dtype=np.int64)
-    return {
+    out = {
         "model.embed_tokens.weight": (emb_idx, emb_rows),
         p + "mlp.gate_proj.weight": (unit_idx, gate),
         p + "mlp.up_proj.weight": (unit_idx, gate),
         p + "mlp.down_proj.weight.T": (unit_idx, down),
     }
+    if not arch.tie_word_embeddings:  # untied (TTS-1-Max): the same rows in the lm_head
+        out["lm_head.weight"] = (emb_idx, emb_rows)
+    return out
 
 
 def apply_chain(weights: dict[str, torch.Tensor], arch: configs.LmArch, spec: ChainSpec) -> None:
