@@ -88,7 +88,8 @@ struct LmWork {
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
   DevBuf sw, sgran, sstate;                         // persistent one-row step: weight stream, granules, seq/done
   bool step_ok = false;                             // the persistent step's stream is packed (lm_step.hip)
-  bool step_on = true;                              // ... and the one-row decode runs it (tts_lm_step_mode)
+  int step_mode = 1;                                // one-row decode: 0 per-layer launches, 1 the whole
+                                                    // persistent step, 2 launches + MLP block (tts_lm_step_mode)
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]

@@ -123,7 +123,7 @@ void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::ve
 
 // The one-row decode step as one persistent launch (lm_step.hip) where the geometry allows
 // it (TTS-1 on 256 CUs), opt-in with TTS_STEP=1 while it is slower than the launches.
-static bool use_step() { return getenv("TTS_STEP") && atoi(getenv("TTS_STEP")); }  // (read at each load)
+static int use_step() { return getenv("TTS_STEP") ? atoi(getenv("TTS_STEP")) : 0; }  // (read at each load)
 
 // the persistent step's hand-off state: granule tags 0xffffffff (never a step's), seq 1, done 0
 static void step_reset(Engine* e, hipStream_t s) {
@@ -179,7 +179,8 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   // the one-row decode step as one persistent launch (lm_step.hip) keeps its own copy of the
   // layer weights in its stream order (1.9 GB for TTS-1)
   LmWork& w = e->w;
-  w.step_ok = use_step() && step_supported(HID, H, KVH, D, FF, L, e->num_cu);
+  w.step_ok = use_step() > 0 && step_supported(HID, H, KVH, D, FF, L, e->num_cu);
+  w.step_mode = use_step() == 2 ? 2 : 1;
   if (w.step_ok) w.sw.alloc(step_stream_bytes(L));
   else w.sw.release();
   // matrix (N_total rows, ng) <- row block of N rows at n-tile offset `off` (or interleaved);
@@ -458,12 +459,13 @@ struct Ctx {
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
-    if (decode && rows == 1 && w.step_ok && w.step_on) {  // the whole one-row stack as one persistent launch
+    if (decode && rows == 1 && w.step_ok && w.step_mode == 1) {  // the whole one-row stack as one persistent launch
       launch_decode_step(step_args(slot, pos), s);
       return;
     }
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
+    const bool mlp_block = decode && rows == 1 && w.step_ok && w.step_mode == 2;
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
@@ -485,6 +487,11 @@ struct Ctx {
         launch_attn_prefill(a, s);
       }
       gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID);
+      if (mlp_block) {  // gate/up + down as one launch on the step engine (lm_step.hip)
+        launch_mlp_block(step_args(slot, pos), l, s);
+        pending_norm = nullptr;
+        continue;
+      }
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
@@ -969,8 +976,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
-  TTS_REQUIRE(which != 7 || (rows == 1 && e->w.step_ok), "the persistent step needs one TTS-1 row");
+  TTS_REQUIRE(which >= 0 && which <= 8 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which < 7 || (rows == 1 && e->w.step_ok), "the persistent step needs one TTS-1 row");
   TTS_REQUIRE(which != 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
   hipStream_t s = e->stream;
   Ctx X(e, s);
@@ -1051,6 +1058,10 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
                                     (double)c.num_kv_heads * ctx * c.head_dim * 2 * 2) +
             act_rw * 2 * HID;
         break;
+      case 8:  // the MLP half of layer li for one row (gate/up + down on the step engine)
+        launch_mlp_block(X.step_args(e->w.row_slot.as<int>(), e->w.row_pos.as<int>()), li, s);
+        b = 2.0 * (2.0 * FF * HID + HID * FF) + act_rw * 2 * HID + 2.0 * HID;
+        break;
     }
   };
   launch();
@@ -1071,10 +1082,10 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
 // stream is packed (TTS_STEP=1 at tts_lm_load on a TTS-1 geometry with 256 CUs).
 void lm_step_mode(Engine* e, int mode, int* available) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
-  TTS_REQUIRE(mode >= -1 && mode <= 1, "bad step mode");
-  TTS_REQUIRE(mode != 1 || e->w.step_ok, "the persistent step is not available for this model");
-  if (mode >= 0 && (mode == 1) != e->w.step_on) {
-    e->w.step_on = mode == 1;
+  TTS_REQUIRE(mode >= -1 && mode <= 2, "bad step mode");
+  TTS_REQUIRE(mode < 1 || e->w.step_ok, "the persistent step is not available for this model");
+  if (mode >= 0 && mode != e->w.step_mode) {
+    e->w.step_mode = mode;
     if (e->w.graph) {
       HIP_CHECK(hipStreamSynchronize(e->stream));
       (void)hipGraphExecDestroy(e->w.graph);
@@ -1092,7 +1103,7 @@ void lm_step_mode(Engine* e, int mode, int* available) {
 // stack (tests/test_gpu_step.py).
 void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
-  TTS_REQUIRE(path >= 0 && path <= 3, "bad probe path");
+  TTS_REQUIRE(path >= 0 && path <= 5, "bad probe path");
   TTS_REQUIRE(path == 0 || e->w.step_ok, "the persistent step is not available for this model");
   TTS_REQUIRE(pos >= 0 && pos < e->lm.cfg.max_seq_len && token >= 0 && token < e->lm.cfg.vocab_size, "bad probe");
   hipStream_t s = e->stream;
@@ -1103,7 +1114,7 @@ void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
   HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, &zero, 4, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(e->w.row_pos.p, &pos, 4, hipMemcpyHostToDevice, s));
   launch_embed(e->w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), 1, HID, s);
-  if (path >= 2) {  // the persistent step with its per-phase stamps: x_out = [layer][CU][kStepEvents] us
+  if (path >= 2 && path <= 4) {  // the persistent step with its per-phase stamps: x_out = [layer][CU][kStepEvents] us
                     // (path 3: every hand-off taken as ready, results garbage: the stream's own pace)
     const size_t n = (size_t)X.c.num_layers * e->num_cu * kStepEvents;
     unsigned long long* tr = nullptr;
@@ -1111,7 +1122,7 @@ void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
     HIP_CHECK(hipMemsetAsync(tr, 0, n * 8, s));
     StepArgs sa = X.step_args(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
     sa.trace = tr;
-    sa.nodeps = path == 3;
+    sa.nodeps = path - 2;
     launch_decode_step(sa, s);
     HIP_CHECK(hipGetLastError());
     std::vector<unsigned long long> t(n);
@@ -1125,16 +1136,16 @@ void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
     check_fattn(e, s);
     return;
   }
-  const bool saved = e->w.step_on;
-  e->w.step_on = path == 1;
+  const int saved = e->w.step_mode;
+  e->w.step_mode = path == 1 ? 1 : path == 5 ? 2 : 0;
   X.layers(1, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
-  e->w.step_on = saved;
+  e->w.step_mode = saved;
   HIP_CHECK(hipGetLastError());
   // x_out: [hidden] residual stream, then the last layer's qkv [QKV] and attention output [H*D]
   const int QKV = X.QKV(), HD = X.c.num_heads * X.c.head_dim;
   std::vector<uint16_t> h(HID + QKV + HD);
   HIP_CHECK(hipMemcpyAsync(h.data(), e->w.x.p, HID * 2, hipMemcpyDeviceToHost, s));
-  if (path == 0) {
+  if (path == 0 || path == 5) {
     HIP_CHECK(hipMemcpyAsync(h.data() + HID, e->w.qkv.p, QKV * 2, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(h.data() + HID + QKV, e->w.attn_out.p, HD * 2, hipMemcpyDeviceToHost, s));
   } else {  // the step's granules of the last layer (lm_step.hip: G_QKV at HID/2, G_ATT after it)

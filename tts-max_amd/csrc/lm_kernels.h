@@ -128,7 +128,7 @@ void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hi
 // ---- the one-row decode step's layers as one persistent launch (lm_step.hip; TTS-1 geometry)
 struct StepArgs {
   static constexpr int kMaxLayers = 32;
-  const void* stream = nullptr;                 // weight stream: [CU][slot][16 KiB] (launch_step_pack)
+  const void* stream = nullptr;                 // weight stream: [slot][CU][16 KiB] (launch_step_pack)
   const bf16_t* ln1 = nullptr;                  // layer 0's RMSNorm weights (input, post-attention);
   const bf16_t* ln2 = nullptr;                  //   layer l's at + l * ln_stride elements
   long long ln_stride = 0;
@@ -155,6 +155,8 @@ bool step_supported(int hidden, int heads, int kv_heads, int head_dim, int ffn, 
 size_t step_stream_bytes(int layers);
 size_t step_gran_elems(int layers);
 void launch_decode_step(const StepArgs& a, hipStream_t s);
+// the MLP half of layer `layer` for one row (h in a.x -> x over it) on the same stream
+void launch_mlp_block(const StepArgs& a, int layer, hipStream_t s);
 // row-major W of one layer's matrix -> the step's weight stream; kind 0 qkv, 1 o, 2 gate, 3 up, 4 down
 void launch_step_pack(const bf16_t* w, void* stream, int kind, int layer, int L, hipStream_t s);
 

@@ -14,13 +14,13 @@
 //     vector from the other CUs, its ring keeps filling with the weights it will multiply
 //     next.
 //   * waves 1..7 are CONSUMERS: slot s of the step goes to consumer s % 7; a slot is a
-//     self-contained piece of work (4 whole rows of a K = 2048 matrix, or 256 outputs of
-//     the CU's K-slice of the down projection), multiplied on the VALU (v_dot2_f32_bf16)
-//     against the op's input vector in LDS once it is there.
+//     self-contained piece of work (4 whole rows of a K = 2048 matrix, or 8 rows of the
+//     down projection over a 1024-wide k chunk), multiplied on the VALU (v_dot2_f32_bf16)
+//     against the op's input vector once it is there.
 // Every CU owns a fixed slice of each matrix: qkv outputs 12c .. 12c+11, o outputs 8c ..
-// 8c+7, gate/up outputs (= act) 32c .. 32c+31, and the down projection's K-slice
-// 32c .. 32c+31 (its own act values, so down starts without waiting for other CUs: each CU
-// publishes a 2048-wide fp32 partial and CU c sums outputs 8c .. 8c+7 over all 256 CUs).
+// 8c+7, gate/up outputs (= act) 32c .. 32c+31 and down outputs 8c .. 8c+7 (the whole
+// K = 8192: down slot t covers k = 1024t .. +1023 and gathers just that act chunk, made by CUs
+// 32t .. 32t+31, so it neither waits for every CU nor needs a cross-CU partial reduction).
 // Vectors move between CUs as 8-byte granules {payload, tag} written by ONE agent-scope
 // store each (tag = the step's sequence number: a granule left by an earlier step never
 // matches) and gathered by one wave per vector per CU (MI355X_MICROARCH.md: granule,
@@ -65,23 +65,23 @@ constexpr int G_X = 0;                   // layer output x_{l+1}: bf16 pairs [HI
 constexpr int G_QKV = G_X + HID / 2;     // q | k | v before RoPE: bf16 pairs [QKVN/2]
 constexpr int G_ATT = G_QKV + QKVN / 2;  // attention output: bf16 pairs [HID/2]
 constexpr int G_H = G_ATT + HID / 2;     // residual after attention: bf16 pairs [HID/2]
-constexpr int G_PD = G_H + HID / 2;      // down partials: f32 [HID/8 blocks][NCU producers][8]
-constexpr int G_LAYER = G_PD + HID * NCU;
+constexpr int G_ACT = G_H + HID / 2;     // SiLU(gate) * up: bf16 pairs [FFN/2]
+constexpr int G_LAYER = G_ACT + FFN / 2;
 
 // LDS carve-up (bytes)
 constexpr int L_RING = 0;
 constexpr int L_X = L_RING + NS * SLOT;       // x_l (bf16 [HID])
 constexpr int L_H = L_X + HID * 2;            // h (bf16 [HID])
 constexpr int L_A = L_H + HID * 2;            // attention output (bf16 [HID])
-constexpr int L_ACT = L_A + HID * 2;          // this CU's act slice (bf16 [32])
-constexpr int L_QS = L_ACT + 64;              // attention: roped q [GQ][HDIM] f32
+constexpr int L_DP = L_A + HID * 2;           // down: the 8 slots' row sums (f32 [S_D][8])
+constexpr int L_QS = L_DP + S_D * 8 * 4;      // attention: roped q [GQ][HDIM] f32
 constexpr int L_RAW = L_QS + GQ * HDIM * 4;   // attention: gathered q | k | v pairs (u32)
 constexpr int L_KN = L_RAW + (GQ * HDIM / 2 + HDIM) * 4;  // new k, new v (bf16 [HDIM] each)
 constexpr int L_AO = L_KN + 2 * HDIM * 2;     // attention output of the group (bf16 [GQ*HDIM])
 constexpr int L_RED = L_AO + GQ * HDIM * 2;   // attention merge scratch
 constexpr int L_FLAGS = L_RED + dec_red_floats<HDIM, NCONS>() * 4;
-constexpr int F_FULL = 0, F_FREE = NS, F_RX = 2 * NS, F_RA = F_RX + 1, F_RH = F_RX + 2, F_ACT = F_RX + 3,
-              F_BAR = F_RX + 4, F_RED = F_RX + 5, F_DD = F_RX + 6, F_N = F_RX + 8;
+constexpr int F_FULL = 0, F_FREE = NS, F_RX = 2 * NS, F_RA = F_RX + 1, F_RH = F_RX + 2, F_BAR = F_RX + 3,
+              F_DS = F_RX + 4, F_XP = F_RX + 5, F_GU = F_RX + 6, F_GATH = F_RX + 7, F_N = F_RX + 8;
 constexpr int LDS_BYTES = L_FLAGS + F_N * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "decode step LDS");
 
@@ -102,6 +102,19 @@ TTS_DEV void gst(uint64_t* p, uint32_t payload, uint32_t tag) {
 }
 TTS_DEV int gerr(const int* e) { return __hip_atomic_load((const gint*)e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 TTS_DEV void set_err(int* e) { __hip_atomic_store((gint*)e, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// The loader's flag accesses as inline asm: the compiler treats any LDS access after an
+// LDS-DMA load as a possible alias of the DMA destination and drains every load in flight
+// (s_waitcnt vmcnt(0)) before it, which would leave one slot in flight.  The ring protocol
+// orders them instead (counted vmcnt before FULL, FREE read before the slot is refilled).
+TTS_DEV int lds_ld_dma(lint* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(size_t)p) : "memory");
+  return v;
+}
+TTS_DEV void lds_st_dma(lint* p, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(size_t)p), "v"(v) : "memory");
+}
 
 // wave-uniform wait until the LDS word reaches v (bounded; err drains every wave)
 TTS_DEV void lds_spin_ge(lint* p, int v, int* err) {
@@ -206,17 +219,20 @@ TTS_DEV void plain_chunks(const bf16_t* v, int lane, u32x4_t (&xn)[4]) {
 
 // the 4 rows of a K = 2048 slot against the lane's chunks: wave-uniform fp32 results
 TTS_DEV void rows4(const char* slot, const u32x4_t (&xn)[4], int lane, float (&y)[4]) {
-  u32x4_t w[4][4];  // all 16 LDS reads in flight before the first product
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int h = 0; h < 2; ++h) {  // two rows at a time: 8 LDS reads in flight before the products
+    u32x4_t w[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[r][j] = *(const u32x4_t*)(slot + r * 4096 + j * 1024 + lane * 16);
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float acc = 0.f;
+      for (int j = 0; j < 4; ++j) w[r][j] = *(const u32x4_t*)(slot + (2 * h + r) * 4096 + j * 1024 + lane * 16);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc = dot8(w[r][j], xn[j], acc);
-    y[r] = wave_sum_dpp(acc);
+    for (int r = 0; r < 2; ++r) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = dot8(w[r][j], xn[j], acc);
+      y[2 * h + r] = wave_sum_dpp(acc);
+    }
   }
 }
 
@@ -235,7 +251,8 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
   };
   const bf16_t* kc = a.kv + 2 * kvl + kvbase;                // K rows of (slot, kv head c)
   const bf16_t* vtc = a.kv + 2 * kvl + a.kv_layer + kvbase;  // V^T columns
-  // this wave's first-pass K / V^T fragments, in flight while q / k / v are gathered
+  // this wave's first-pass K / V^T fragments, in flight while q / k / v are gathered (loading
+  // them earlier, at the top of the layer, keeps them live across the slot math: spills)
   using C = DecShape<HDIM, PW>;
   u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
   if (cw * PW < ctx) {
@@ -248,6 +265,10 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
   bf16_t* knew = (bf16_t*)(smem + L_KN);
   bf16_t* vnew = knew + HDIM;
   bf16_t* ao = (bf16_t*)(smem + L_AO);
+  // the RoPE table entries too (a dependent global load after the gather would sit on the
+  // critical path)
+  const int qd = ctid % HDIM;
+  const float qc = bf2f(a.rope_cos[(size_t)pos * HDIM + qd]), qsn = bf2f(a.rope_sin[(size_t)pos * HDIM + qd]);
   constexpr int NQ = GQ * HDIM / 2, NG = NQ + HDIM;
   if (ctid < NG) {
     int col;
@@ -258,8 +279,6 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
   }
   cbar();
   if (cw == 0 && lane == 0) stamp(a.trace, l, c, 14);
-  const int qd = ctid % HDIM;
-  const float qc = bf2f(a.rope_cos[(size_t)pos * HDIM + qd]), qsn = bf2f(a.rope_sin[(size_t)pos * HDIM + qd]);
   constexpr int H2 = HDIM / 2;
   if (ctid < GQ * HDIM) {
     const int g = ctid / HDIM;
@@ -283,26 +302,28 @@ TTS_DEV void step_attention(const StepArgs& a, char* smem, uint64_t* G, uint32_t
 }
 
 // The loader wave: this CU's weight stream through the LDS ring (see the header).
-__attribute__((noinline)) __device__ void step_loader(const void* stream, char* smem, int c, int lane, int total,
-                                                      int* err, unsigned long long* tr) {
+__attribute__((noinline)) __device__ void step_loader(const void* stream, char* smem, int c, int lane, int s_begin,
+                                                      int total, int* err, unsigned long long* tr) {
   lint* fl = lflags(smem);
-  const char* src = (const char*)stream + (size_t)c * total * SLOT;
-  int pub = 0;  // first slot not yet published (slots pub .. s-1 are in flight)
+  // slot-major stream [slot][CU][16 KiB]: at any moment the 256 loaders read one contiguous
+  // 4 MiB window (few pages, few DRAM rows) instead of 256 scattered per-CU regions
+  const char* src = (const char*)stream + (size_t)c * SLOT;
+  int pub = s_begin;  // first slot not yet published (slots pub .. s-1 are in flight)
   int spins = 0;
   bool bad = false;
 #pragma unroll 1
-  for (int s = 0; s < total; ++s) {
+  for (int s = s_begin; s < total; ++s) {
     const int r = s % NS;
     if (tr && lane == 0 && s % S_LAYER == 0) stamp(tr, s / S_LAYER, c, 12);
     // ring full: while the slot is still being read, publish the in-flight slots as they land
     // (oldest first, the newer ones stay in flight)
-    while (lds_ld(fl + F_FREE + r) != s - NS) {
+    while (lds_ld_dma(fl + F_FREE + r) != s - NS) {
       const int inflight = s - pub;
       if (inflight > 0) {
         if (inflight >= 3) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
         else if (inflight == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_st(fl + F_FULL + pub % NS, pub);
+        lds_st_dma(fl + F_FULL + pub % NS, pub);
         ++pub;
         continue;
       }
@@ -316,19 +337,24 @@ __attribute__((noinline)) __device__ void step_loader(const void* stream, char* 
     }
     if (bad) break;
     spins = 0;
-    const char* gs = src + (size_t)s * SLOT + lane * 16;
+    const char* gs = src + (size_t)s * NCU * SLOT + lane * 16;
     char* ls = smem + L_RING + r * SLOT;
 #pragma unroll
     for (int p = 0; p < SLOT / 1024; ++p)
       __builtin_amdgcn_global_load_lds((gptr_t)(gs + p * 1024), (lptr_t)(ls + p * 1024), 16, 0, 2 /* nt */);
-    if (s - pub + 1 > FLY) {  // the oldest in-flight slot has landed once FLY newer ones remain
+    if (lds_ld_dma(fl + F_GATH) > 0) {
+      // a wave of this CU is sweeping granules: thin the stream to this one slot in flight so
+      // the sweep's loads do not queue behind a refill burst (MI355X_MICROARCH.md gather-pass)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      for (; pub < s; ++pub) lds_st_dma(fl + F_FULL + pub % NS, pub);
+    } else if (s - pub + 1 > FLY) {  // the oldest in-flight slot has landed once FLY newer ones remain
       asm volatile("s_waitcnt vmcnt(48)" ::: "memory");  // = FLY * 16 loads
-      lds_st(fl + F_FULL + pub % NS, pub);
+      lds_st_dma(fl + F_FULL + pub % NS, pub);
       ++pub;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (; pub < total; ++pub) lds_st(fl + F_FULL + pub % NS, pub);
+  for (; pub < total; ++pub) lds_st_dma(fl + F_FULL + pub % NS, pub);
 }
 
 }  // namespace
@@ -347,7 +373,7 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
   __syncthreads();  // (the only workgroup barrier: the loader runs free from here on)
 
   if (wave == 0) {
-    step_loader(a.stream, smem, c, lane, total, a.err, a.trace);
+    step_loader(a.stream, smem, c, lane, 0, total, a.err, a.trace);
     return;
   }
 
@@ -356,7 +382,6 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
   bf16_t* xs = (bf16_t*)(smem + L_X);
   bf16_t* hs = (bf16_t*)(smem + L_H);
   bf16_t* as = (bf16_t*)(smem + L_A);
-  bf16_t* act = (bf16_t*)(smem + L_ACT);
   const bool attn_cu = c < NKV;  // kv head c
   const int pos = a.row_pos[0], ctx = pos + 1, slot_kv = a.row_slot[0];
   int nbar = 0;
@@ -391,6 +416,13 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
     const size_t kvl = (size_t)l * a.kv_layer;
     const size_t kvbase = ((size_t)slot_kv * NKV + c) * a.kv_stride * HDIM;
 
+    if (a.nodeps == 2) {  // diagnostics: the loader's own pace (slots released unread)
+      if (cw == 0) EV(0);
+#pragma unroll 1
+      for (int t = 0; t < S_LAYER; ++t)
+        if ((base + t) % NCONS == cw) on_slot(base + t, [](const char*) {});
+      continue;
+    }
     // 1. x_l: the token embedding (layer 0, written by the previous step's finalize) or the
     //    previous layer's output granules
     if (cw == 0) {
@@ -401,8 +433,10 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
       } else {
         // sweep once this CU's own part of x_l is out: by then the other CUs' parts are
         // close, and the sweep's loads no longer queue beside this CU's down stream
-        lds_wait_ge(fl + F_RED, 4 * l, a.err);
+        lds_wait_ge(fl + F_XP, l, a.err);
+        if (lane == 0) lds_add(fl + F_GATH, 1);
         gather_vec(Gprev + G_X, tag, xs, lane, a.err, a.nodeps);
+        if (lane == 0) lds_add(fl + F_GATH, -1);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) lds_st(fl + F_RX, l + 1);
@@ -434,7 +468,9 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
     }
     // 4. the attention output of all heads
     if (cw == 1) {
+      if (lane == 0) lds_add(fl + F_GATH, 1);
       gather_vec(G + G_ATT, tag, as, lane, a.err, a.nodeps);
+      if (lane == 0) lds_add(fl + F_GATH, -1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) lds_st(fl + F_RA, l + 1);
       EV(4);
@@ -463,12 +499,15 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
     }
     // 6. h of all columns
     if (cw == 2) {
+      if (lane == 0) lds_add(fl + F_GATH, 1);
       gather_vec(G + G_H, tag, hs, lane, a.err, a.nodeps);
+      if (lane == 0) lds_add(fl + F_GATH, -1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) lds_st(fl + F_RH, l + 1);
       EV(6);
     }
-    // 7. gate/up slots: act 32c + 2t, +1 = SiLU(gate) * up (bf16), RMSNorm(h, ln2) on the fly
+    // 7. gate/up slots: act 32c + 2t, +1 = SiLU(gate) * up (bf16), RMSNorm(h, ln2) on the fly,
+    //    published for the down slots of every CU
     {
       bool have = false;
       u32x4_t xn[4];
@@ -483,98 +522,86 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
           rows4(sl, xn, lane, y);
           if (lane == 0) {
             const float a0 = rbf(rbf(silu_f(rbf(y[0]))) * rbf(y[2])), a1 = rbf(rbf(silu_f(rbf(y[1]))) * rbf(y[3]));
-            ((uint32_t*)act)[t] = pack_bf2(a0, a1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lds_add(fl + F_ACT, 1);
+            gst(G + G_ACT + 16 * c + t, pack_bf2(a0, a1), tag);
           }
         });
+        if (lane == 0) lds_add(fl + F_GU, 1);
         if (t == S_GU - 1) EV(7);
       }
     }
-    // 8. down slots: this CU's K-slice (its 32 act values) against 256 outputs per slot,
-    //    fp32 partials published for the column owners
+    // 8. down slots: slot t = this CU's 8 output rows 8c .. 8c+7 over k = 1024 t .. +1023;
+    //    its act chunk (produced by CUs 32t .. 32t+31) gathered straight into registers while
+    //    the slot itself is already in the ring.  The last slot to finish sums the 8 chunks in
+    //    order, adds h and publishes this CU's part of x_{l+1}.
     {
-      bool have = false;
-      u32x4_t av[4];
 #pragma unroll 1
       for (int t = 0; t < S_D; ++t) {
         const int s = base + O_D + t;
         if (s % NCONS != cw) continue;
-        lds_wait_ge(fl + F_ACT, S_GU * (l + 1), a.err);
+        // sweep once this CU's own gate/up slots are done (the other CUs' are then close, and
+        // the sweep no longer queues beside this CU's gate/up stream)
+        lds_wait_ge(fl + F_GU, S_GU * (l + 1), a.err);
         if (t == 0) EV(8);
-        if (!have) {
+        // act k = 1024 t + 8 lane + 512 j + e  ->  granule 512 t + 4 lane + 256 j + e / 2
+        const uint64_t* ga = G + G_ACT + 512 * t + 4 * lane;
+        if (lane == 0) lds_add(fl + F_GATH, 1);
+        uint64_t gv[8];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) av[i] = *(const u32x4_t*)(act + 8 * i);
-          have = true;
+        for (int k = 0; k < 8; ++k) gv[k] = gld(ga + 256 * (k >> 2) + (k & 3));
+        uint32_t pending = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pending |= ((uint32_t)(gv[k] >> 32) != tag && !a.nodeps) ? 1u << k : 0u;
+        int spins = 0;
+        while (pending) {
+          if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(a.err))) {
+            set_err(a.err);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (pending & (1u << k)) gv[k] = gld(ga + 256 * (k >> 2) + (k & 3));
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if ((uint32_t)(gv[k] >> 32) == tag) pending &= ~(1u << k);
         }
-        on_slot(s, [&](const char* sl) {
-          u32x4_t w[4][4];
+        if (lane == 0) lds_add(fl + F_GATH, -1);
+        u32x4_t av[2];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
+        for (int k = 0; k < 8; ++k) av[k >> 2][k & 3] = (uint32_t)gv[k];
+        float* dp = (float*)(smem + L_DP);
+        on_slot(s, [&](const char* sl) {  // slot layout [row 8][k 1024]
+          u32x4_t w[8][2];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) w[q][i] = *(const u32x4_t*)(sl + i * 4096 + (lane + 64 * q) * 16);
+          for (int r = 0; r < 8; ++r)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int nn = lane + 64 * q;  // slot layout [i][256 n][8]
-            float acc = 0.f;
+            for (int j = 0; j < 2; ++j) w[r][j] = *(const u32x4_t*)(sl + r * 2048 + j * 1024 + lane * 16);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc = dot8(w[q][i], av[i], acc);
-            const int n = 256 * t + nn;
-            gst(G + G_PD + ((size_t)(n >> 3) * NCU + c) * 8 + (n & 7), __float_as_uint(acc), tag);
+          for (int r = 0; r < 8; ++r) {
+            const float y = wave_sum_dpp(dot8(w[r][1], av[1], dot8(w[r][0], av[0], 0.f)));
+            if (lane == 0) dp[8 * t + r] = y;
           }
         });
-        if (lane == 0) lds_add(fl + F_DD, 1);
-        if (t == S_D - 1) EV(9);
-      }
-    }
-    // 9. column owner: outputs 8c .. 8c+7 = sum over the 256 producers (fixed order), rounded,
-    //    added to h -> x_{l+1} published (and, after the last layer, written for the lm_head)
-    if (cw >= NCONS - 4) {
-      const int j0 = 2 * (cw - (NCONS - 4));  // columns 8c + j0, 8c + j0 + 1
-      // the 2 x 4 partials of this lane's producers 4 lane .. 4 lane + 3, re-swept together,
-      // first swept once this CU's own down slots are done (polling earlier would slow this
-      // CU's own weight stream for the slots still to come)
-      lds_wait_ge(fl + F_DD, S_D * (l + 1), a.err);
-      const uint64_t* pd = G + G_PD + (size_t)c * NCU * 8 + j0 + lane * 32;
-      float v[2][4];
-      uint64_t gv[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) gv[k] = gld(pd + (k & 3) * 8 + (k >> 2));
-      uint32_t pending = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) pending |= ((uint32_t)(gv[k] >> 32) != tag && !a.nodeps) ? 1u << k : 0u;
-      int spins = 0;
-      while (pending) {
-        if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(a.err))) {
-          set_err(a.err);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (pending & (1u << k)) gv[k] = gld(pd + (k & 3) * 8 + (k >> 2));
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if ((uint32_t)(gv[k] >> 32) == tag) pending &= ~(1u << k);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k >> 2][k & 3] = __uint_as_float((uint32_t)gv[k]);
-      const float d0 = wave_sum_dpp((v[0][0] + v[0][1]) + (v[0][2] + v[0][3]));
-      const float d1 = wave_sum_dpp((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
-      if (j0 == 0) EV(10);
-      float* red = (float*)(smem + L_RED);  // (attention scratch: free by now)
-      if (lane == 0) {
-        red[j0] = rbf(bf2f(hs[8 * c + j0]) + rbf(d0));
-        red[j0 + 1] = rbf(bf2f(hs[8 * c + j0 + 1]) + rbf(d1));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lds_add(fl + F_RED, 1) == 4 * (l + 1) - 1) {  // the last of the 4 publishes
-          EV(11);
-          for (int k = 0; k < 4; ++k) {
-            const float x0 = red[2 * k], x1 = red[2 * k + 1];
-            gst(G + G_X + 4 * c + k, pack_bf2(x0, x1), tag);
-            if (l == L - 1) ((uint32_t*)a.x)[4 * c + k] = pack_bf2(x0, x1);
+        if (lane == 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lds_add(fl + F_DS, 1) == S_D * (l + 1) - 1) {  // the last slot: x_{l+1} = h + down
+            EV(11);
+            for (int k = 0; k < 4; ++k) {
+              float xv[2];
+              for (int e = 0; e < 2; ++e) {
+                const int r = 2 * k + e;
+                float d = 0.f;
+                for (int u = 0; u < S_D; ++u) d += dp[8 * u + r];
+                xv[e] = rbf(bf2f(hs[8 * c + r]) + rbf(d));
+              }
+              gst(G + G_X + 4 * c + k, pack_bf2(xv[0], xv[1]), tag);
+              if (l == L - 1) ((uint32_t*)a.x)[4 * c + k] = pack_bf2(xv[0], xv[1]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_add(fl + F_XP, 1);
           }
         }
+        if (t == S_D - 1) EV(9);
       }
     }
     if (gerr(a.err)) break;
@@ -582,6 +609,136 @@ __global__ __launch_bounds__(NWV * 64) void decode_step_kernel(StepArgs a) {
 #undef EV
   // the last CU out advances the step tag for the next replay
   if (tid == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (__hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NCU - 1) {
+      __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.seq, (int)(tag + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ MLP block ---------
+// The MLP half of ONE layer of the one-row decode as one launch on the same engine and weight
+// stream (the per-layer launch path's gate/up + down pair): h = the residual after attention
+// (row 0 of a.x, written by the o_proj launch before this one), RMSNorm(h, ln2) -> gate/up
+// slots -> act granules -> down slots (each gathers its act chunk from 32 CUs while its
+// weights are already in the ring) -> x = h + down written back over h.  In place is safe:
+// a CU writes its 8 outputs only after it has gathered act from every CU, and every CU read
+// all of h before it published act.  The launch boundary carries x to the next layer (no
+// granule all-gather), and the down weights stream in while act is exchanged.
+__global__ __launch_bounds__(NWV * 64) void mlp_block_kernel(StepArgs a, int l) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lint* fl = lflags(smem);
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s_begin = S_LAYER * l + O_GU, s_end = S_LAYER * l + S_LAYER;
+  const uint32_t tag = (uint32_t)__hip_atomic_load(a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < F_N) {  // full / free of ring position r: the slot NS before the first one there
+    int v = 0;
+    if (tid < 2 * NS) {
+      const int r = tid % NS;
+      v = s_begin + ((r - s_begin % NS) + NS) % NS - NS;
+    }
+    fl[tid] = v;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    step_loader(a.stream, smem, c, lane, s_begin, s_end, a.err, nullptr);
+    return;
+  }
+  const int cw = wave - 1;
+  uint64_t* G = a.gran + (size_t)l * G_LAYER;
+  const bf16_t* h = a.x;
+  auto on_slot = [&](int s, auto f) {
+    const int r = s % NS;
+    lds_wait_ge(fl + F_FULL + r, s, a.err);
+    f(smem + L_RING + r * SLOT);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) lds_st(fl + F_FREE + r, s);
+  };
+  // gate/up slots: act 32c + 2t, +1
+  {
+    bool have = false;
+    u32x4_t xn[4];
+#pragma unroll 1
+    for (int t = 0; t < S_GU; ++t) {
+      const int s = s_begin + t;
+      if (s % NCONS != cw) continue;
+      if (!have) { norm_chunks(h, a.ln2 + l * a.ln_stride, a.eps, lane, xn); have = true; }
+      on_slot(s, [&](const char* sl) {
+        float y[4];
+        rows4(sl, xn, lane, y);
+        if (lane == 0) {
+          const float a0 = rbf(rbf(silu_f(rbf(y[0]))) * rbf(y[2])), a1 = rbf(rbf(silu_f(rbf(y[1]))) * rbf(y[3]));
+          gst(G + G_ACT + 16 * c + t, pack_bf2(a0, a1), tag);
+        }
+      });
+      if (lane == 0) lds_add(fl + F_GU, 1);
+    }
+  }
+  // down slots (as in decode_step_kernel), x written back over h
+  float hres[8];
+#pragma unroll 1
+  for (int t = 0; t < S_D; ++t) {
+    const int s = s_begin + (O_D - O_GU) + t;
+    if (s % NCONS != cw) continue;
+    lds_wait_ge(fl + F_GU, S_GU, a.err);
+    const uint64_t* ga = G + G_ACT + 512 * t + 4 * lane;
+    uint64_t gv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] = gld(ga + 256 * (k >> 2) + (k & 3));
+    uint32_t pending = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pending |= ((uint32_t)(gv[k] >> 32) != tag) ? 1u << k : 0u;
+    int spins = 0;
+    while (pending) {
+      if (++spins > MAX_SPINS || ((spins & 255) == 0 && gerr(a.err))) {
+        set_err(a.err);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (pending & (1u << k)) gv[k] = gld(ga + 256 * (k >> 2) + (k & 3));
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((uint32_t)(gv[k] >> 32) == tag) pending &= ~(1u << k);
+    }
+    u32x4_t av[2];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) av[k >> 2][k & 3] = (uint32_t)gv[k];
+    float* dp = (float*)(smem + L_DP);
+    on_slot(s, [&](const char* sl) {
+      u32x4_t w[8][2];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) w[r][j] = *(const u32x4_t*)(sl + r * 2048 + j * 1024 + lane * 16);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float y = wave_sum_dpp(dot8(w[r][1], av[1], dot8(w[r][0], av[0], 0.f)));
+        if (lane == 0) dp[8 * t + r] = y;
+      }
+    });
+    if (lane == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lds_add(fl + F_DS, 1) == S_D - 1) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) hres[r] = bf2f(h[8 * c + r]);
+        for (int k = 0; k < 4; ++k) {
+          float xv[2];
+          for (int e = 0; e < 2; ++e) {
+            const int r = 2 * k + e;
+            float d = 0.f;
+            for (int u = 0; u < S_D; ++u) d += dp[8 * u + r];
+            xv[e] = rbf(hres[r] + rbf(d));
+          }
+          ((uint32_t*)a.x)[4 * c + k] = pack_bf2(xv[0], xv[1]);
+        }
+      }
+    }
+  }
+  if (tid == 64) {  // the last CU out advances the tag
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (__hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NCU - 1) {
       __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -600,22 +757,24 @@ size_t step_gran_elems(int layers) { return (size_t)G_LAYER * layers; }
 void launch_decode_step(const StepArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(decode_step_kernel, dim3(NCU), dim3(NWV * 64), LDS_BYTES, s, a);
 }
+void launch_mlp_block(const StepArgs& a, int layer, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_block_kernel, dim3(NCU), dim3(NWV * 64), LDS_BYTES, s, a, layer);
+}
 
 // ------------------------------------------------------------------ weight stream ------
 // Row-major W of one layer's matrix -> this engine's slots (every CU's share, in stream
 // order).  kind 0 qkv [3072][2048], 1 o [2048][2048], 2 gate [8192][2048], 3 up, 4 down
 // [2048][8192].  One thread = 16 bytes.
 __global__ void step_pack_kernel(const bf16_t* __restrict__ w, char* __restrict__ stream, int kind, int layer, int L) {
-  const size_t total_slots = (size_t)S_LAYER * L;
   const long long n16 = (kind == 0) ? (long long)QKVN * HID / 8 : (kind == 1) ? (long long)HID * HID / 8
                         : (kind == 4) ? (long long)HID * FFN / 8 : (long long)FFN * HID / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
     int cu, s, off;
-    if (kind == 4) {  // Wd[n][k]: CU = k / 32, slot t = n / 256, layout [i = (k%32)/8][nn = n%256][8]
+    if (kind == 4) {  // Wd[n][k]: CU = n / 8, slot t = k / 1024, layout [row n % 8][k % 1024]
       const int n = (int)(i / (FFN / 8)), k = (int)(i % (FFN / 8)) * 8;
-      cu = k / 32;
-      s = O_D + n / 256;
-      off = ((k % 32) / 8) * 4096 + (n % 256) * 16;
+      cu = n / 8;
+      s = O_D + k / 1024;
+      off = (n % 8) * 2048 + (k % 1024) * 2;
     } else {
       const int row = (int)(i / (HID / 8)), k = (int)(i % (HID / 8)) * 8;
       int t, r;
@@ -629,7 +788,7 @@ __global__ void step_pack_kernel(const bf16_t* __restrict__ w, char* __restrict_
       }
       off = r * 4096 + k * 2;
     }
-    char* dst = stream + ((size_t)cu * total_slots + (size_t)S_LAYER * layer + s) * SLOT + off;
+    char* dst = stream + (((size_t)S_LAYER * layer + s) * NCU + cu) * SLOT + off;
     *(u32x4_t*)dst = *(const u32x4_t*)(w + i * 8);
   }
 }
