@@ -193,21 +193,6 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes);
 
-/* The one-row decode path: mode 1 = the persistent step (lm_step.hip: every layer as one
- * launch on a weight-streaming engine; its stream is packed at tts_lm_load when TTS_STEP=1
- * and the geometry is TTS-1 on 256 CUs), 0 = the per-layer launches, -1 = query only.
- * available (may be NULL) = whether the persistent step can run. */
-tts_status tts_lm_step_mode(tts_engine* e, int32_t mode, int32_t* available);
-
-/* Diagnostics: one decode-step pass of the layer stack for one row (the embedding of `token`
- * at position `pos` of KV slot 0, the cache as it stands): path 1 = the persistent one-row
- * step (lm_step.hip; TTS-1 geometry), 0 = the per-layer launches.  x_out (host fp32
- * [hidden + qkv width + heads * head_dim]) = the residual stream after the last layer (before
- * the final RMSNorm), then the last layer's q|k|v (before RoPE) and attention output.
- * path 2 (3: hand-offs not awaited, results meaningless) = the persistent step with its phase stamps: x_out (fp32 [layers][CUs][16]) = the
- * microseconds of each phase event since the first stamp (-1 = not stamped on that CU). */
-tts_status tts_lm_step_probe(tts_engine* e, int32_t token, int32_t pos, int32_t path, float* x_out);
-
 /* ---------------------------------------------------------------------- codec ------ */
 
 /* xcodec2-compatible decoder (tts/core/codec/decoding.py:14-35 DecoderConfig). */

@@ -228,26 +228,6 @@ tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32
   });
 }
 
-tts_status tts_lm_step_mode(tts_engine* e, int32_t mode, int32_t* available) {
-  return guarded([&] {
-    TTS_REQUIRE(e, "null argument");
-    Engine* E = reinterpret_cast<Engine*>(e);
-    HIP_CHECK(hipSetDevice(E->device));
-    int av = 0;
-    lm_step_mode(E, mode, &av);
-    if (available) *available = av;
-  });
-}
-
-tts_status tts_lm_step_probe(tts_engine* e, int32_t token, int32_t pos, int32_t path, float* x_out) {
-  return guarded([&] {
-    TTS_REQUIRE(e && x_out, "null argument");
-    Engine* E = reinterpret_cast<Engine*>(e);
-    HIP_CHECK(hipSetDevice(E->device));
-    lm_step_probe(E, token, pos, path, x_out);
-  });
-}
-
 tts_status tts_codec_load(tts_engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t,
                           int32_t n) {
   return guarded([&] {

@@ -86,10 +86,6 @@ struct LmWork {
   DevBuf blocks;                                    // prefill query blocks (int4, lm_attn.hip)
   int nblocks = 0;
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
-  DevBuf sw, sgran, sstate;                         // persistent one-row step: weight stream, granules, seq/done
-  bool step_ok = false;                             // the persistent step's stream is packed (lm_step.hip)
-  int step_mode = 1;                                // one-row decode: 0 per-layer launches, 1 the whole
-                                                    // persistent step, 2 launches + MLP block (tts_lm_step_mode)
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
@@ -163,8 +159,6 @@ void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_l
               float* logits, hipStream_t s);
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes);
-void lm_step_mode(Engine* e, int mode, int* available);
-void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out);
 
 // upload a named tensor to device memory as bf16 (convert from f32 if needed)
 void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging);

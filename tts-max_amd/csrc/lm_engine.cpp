@@ -121,19 +121,6 @@ void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::ve
 }
 }  // namespace
 
-// The one-row decode step as one persistent launch (lm_step.hip) where the geometry allows
-// it (TTS-1 on 256 CUs), opt-in with TTS_STEP=1 while it is slower than the launches.
-static int use_step() { return getenv("TTS_STEP") ? atoi(getenv("TTS_STEP")) : 0; }  // (read at each load)
-
-// the persistent step's hand-off state: granule tags 0xffffffff (never a step's), seq 1, done 0
-static void step_reset(Engine* e, hipStream_t s) {
-  LmWork& w = e->w;
-  HIP_CHECK(hipMemsetAsync(w.sgran.p, 0xff, w.sgran.bytes, s));
-  const int st[2] = {1, 0};
-  HIP_CHECK(hipMemcpyAsync(w.sstate.p, st, 8, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-}
-
 void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int n) {
   TTS_REQUIRE(cfgp != nullptr, "null config");
   const tts_lm_config c = *cfgp;
@@ -176,49 +163,28 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
 
   DevBuf staging, staging32;
   staging.alloc((size_t)std::max<size_t>((size_t)V * HID, (size_t)FF * HID) * 2);
-  // the one-row decode step as one persistent launch (lm_step.hip) keeps its own copy of the
-  // layer weights in its stream order (1.9 GB for TTS-1)
-  LmWork& w = e->w;
-  w.step_ok = use_step() > 0 && step_supported(HID, H, KVH, D, FF, L, e->num_cu);
-  w.step_mode = use_step() == 2 ? 2 : 1;
-  if (w.step_ok) w.sw.alloc(step_stream_bytes(L));
-  else w.sw.release();
-  // matrix (N_total rows, ng) <- row block of N rows at n-tile offset `off` (or interleaved);
-  // pack >= 0: also into the step's stream as that kind of matrix of layer `layer`
+  // matrix (N_total rows, ng) <- row block of N rows at n-tile offset `off` (or interleaved)
   const int ncu = e->num_cu;
   auto retiled = [&](const tts_tensor_desc& d, bf16_t* dst, int N, int K, int N_total, int ng,
-                     int mult, int off, int pack = -1, int layer = 0) {
+                     int mult, int off) {
     upload_bf16(d, staging.as<bf16_t>(), s, staging32);
     launch_retile(staging.as<bf16_t>(), dst, N, K, N_total, ng, ncu, s, mult, off);
     HIP_CHECK(hipGetLastError());
-    if (pack >= 0 && w.step_ok) {
-      launch_step_pack(staging.as<bf16_t>(), w.sw.p, pack, layer, L, s);
-      HIP_CHECK(hipGetLastError());
-    }
   };
   for (int l = 0; l < L; ++l) {
     LmLayer& ly = M.layers[l];
     const std::string pre = "model.layers." + std::to_string(l) + ".";
     upload_bf16(tm.get(pre + "input_layernorm.weight", {HID}), ly.ln1, s, staging32);
     upload_bf16(tm.get(pre + "post_attention_layernorm.weight", {HID}), ly.ln2, s, staging32);
-    if (w.step_ok) {  // q | k | v rows of the step's qkv matrix: one packed upload
-      upload_bf16(tm.get(pre + "self_attn.q_proj.weight", {H * D, HID}), staging.as<bf16_t>(), s, staging32);
-      upload_bf16(tm.get(pre + "self_attn.k_proj.weight", {KVH * D, HID}),
-                  staging.as<bf16_t>() + (size_t)H * D * HID, s, staging32);
-      upload_bf16(tm.get(pre + "self_attn.v_proj.weight", {KVH * D, HID}),
-                  staging.as<bf16_t>() + (size_t)(H + KVH) * D * HID, s, staging32);
-      launch_step_pack(staging.as<bf16_t>(), w.sw.p, 0, l, L, s);
-      HIP_CHECK(hipGetLastError());
-    }
     retiled(tm.get(pre + "self_attn.q_proj.weight", {H * D, HID}), ly.wqkv, H * D, HID, QKV, 1, 1, 0);
     retiled(tm.get(pre + "self_attn.k_proj.weight", {KVH * D, HID}), ly.wqkv, KVH * D, HID, QKV, 1, 1,
             H * D / 16);
     retiled(tm.get(pre + "self_attn.v_proj.weight", {KVH * D, HID}), ly.wqkv, KVH * D, HID, QKV, 1, 1,
             (H + KVH) * D / 16);
-    retiled(tm.get(pre + "self_attn.o_proj.weight", {HID, H * D}), ly.wo, HID, H * D, HID, 1, 1, 0, 1, l);
-    retiled(tm.get(pre + "mlp.gate_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2 * FF, 2, 2, 0, 2, l);
-    retiled(tm.get(pre + "mlp.up_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2 * FF, 2, 2, 1, 3, l);
-    retiled(tm.get(pre + "mlp.down_proj.weight", {HID, FF}), ly.wd, HID, FF, HID, 1, 1, 0, 4, l);
+    retiled(tm.get(pre + "self_attn.o_proj.weight", {HID, H * D}), ly.wo, HID, H * D, HID, 1, 1, 0);
+    retiled(tm.get(pre + "mlp.gate_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2 * FF, 2, 2, 0);
+    retiled(tm.get(pre + "mlp.up_proj.weight", {FF, HID}), ly.wgu, FF, HID, 2 * FF, 2, 2, 1);
+    retiled(tm.get(pre + "mlp.down_proj.weight", {HID, FF}), ly.wd, HID, FF, HID, 1, 1, 0);
   }
   upload_bf16(tm.get("model.norm.weight", {HID}), M.final_norm, s, staging32);
   const tts_tensor_desc& emb = tm.get("model.embed_tokens.weight", {V, HID});
@@ -252,6 +218,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   HIP_CHECK(hipStreamSynchronize(s));
 
   // ---- workspaces
+  LmWork& w = e->w;
   if (w.graph) { (void)hipGraphExecDestroy(w.graph); w.graph = nullptr; w.graph_batch = -1; }
   const int B = c.max_batch, S = c.max_seq_len;
   const int R = std::max(B, std::min(kMaxPrefillRows, B * S));
@@ -273,14 +240,6 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
-  if (w.step_ok) {
-    w.sgran.alloc(step_gran_elems(L) * 8);
-    w.sstate.alloc(64);
-    step_reset(e, s);
-  } else {
-    w.sgran.release();
-    w.sstate.release();
-  }
   {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
     const int kmax = std::max(HID, std::max(FF, H * D));
     w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
@@ -433,39 +392,11 @@ struct Ctx {
     return fx;
   }
 
-  StepArgs step_args(const int* slot, const int* pos) {
-    StepArgs a;
-    a.stream = w.sw.p;
-    a.ln1 = M.layers[0].ln1;
-    a.ln2 = M.layers[0].ln2;
-    a.ln_stride = c.num_layers > 1 ? (long long)(M.layers[1].ln1 - M.layers[0].ln1) : 0;  // (one slab per layer)
-    a.L = c.num_layers;
-    a.eps = c.rms_norm_eps;
-    a.scale = (float)(1.0 / sqrt((double)c.head_dim));
-    a.x = w.x.as<bf16_t>();
-    a.kv = w.kv.as<bf16_t>();
-    a.kv_layer = (long long)c.max_batch * c.num_kv_heads * w.kv_stride * c.head_dim;
-    a.kv_stride = w.kv_stride;
-    a.row_slot = slot; a.row_pos = pos;
-    a.rope_cos = M.rope.as<bf16_t>();
-    a.rope_sin = a.rope_cos + (size_t)c.max_seq_len * c.head_dim;
-    a.gran = w.sgran.as<uint64_t>();
-    a.seq = w.sstate.as<int>();
-    a.done = a.seq + 1;
-    a.err = w.ferr.as<int>();
-    return a;
-  }
-
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
-    if (decode && rows == 1 && w.step_ok && w.step_mode == 1) {  // the whole one-row stack as one persistent launch
-      launch_decode_step(step_args(slot, pos), s);
-      return;
-    }
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
-    const bool mlp_block = decode && rows == 1 && w.step_ok && w.step_mode == 2;
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
@@ -487,11 +418,6 @@ struct Ctx {
         launch_attn_prefill(a, s);
       }
       gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID);
-      if (mlp_block) {  // gate/up + down as one launch on the step engine (lm_step.hip)
-        launch_mlp_block(step_args(slot, pos), l, s);
-        pending_norm = nullptr;
-        continue;
-      }
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
@@ -770,7 +696,6 @@ static void check_fattn(Engine* e, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
   if (err) {
     HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 4, s));
-    if (e->w.step_ok) step_reset(e, s);
     HIP_CHECK(hipStreamSynchronize(s));
     TTS_REQUIRE(false, "fused QKV+attention: a granule wait timed out (results invalid)");
   }
@@ -976,8 +901,7 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 8 && iters >= 1, "bad kernel selector");
-  TTS_REQUIRE(which < 7 || (rows == 1 && e->w.step_ok), "the persistent step needs one TTS-1 row");
+  TTS_REQUIRE(which >= 0 && which <= 6 && iters >= 1, "bad kernel selector");
   TTS_REQUIRE(which != 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
   hipStream_t s = e->stream;
   Ctx X(e, s);
@@ -1051,17 +975,6 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
             (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2;
         break;
       }
-      case 7:  // every layer of the one-row step as the persistent launch: all layers' weights,
-               // the K/V of ctx positions per layer, the new position's K/V, the row in / out
-        launch_decode_step(X.step_args(e->w.row_slot.as<int>(), e->w.row_pos.as<int>()), s);
-        b = (double)c.num_layers * (2.0 * (QKV * HID + HID * HD + 2.0 * FF * HID + HID * FF) + 4.0 * HID +
-                                    (double)c.num_kv_heads * ctx * c.head_dim * 2 * 2) +
-            act_rw * 2 * HID;
-        break;
-      case 8:  // the MLP half of layer li for one row (gate/up + down on the step engine)
-        launch_mlp_block(X.step_args(e->w.row_slot.as<int>(), e->w.row_pos.as<int>()), li, s);
-        b = 2.0 * (2.0 * FF * HID + HID * FF) + act_rw * 2 * HID + 2.0 * HID;
-        break;
     }
   };
   launch();
@@ -1075,95 +988,6 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   *avg_ms = ms / iters;
   *bytes = b;
   check_fattn(e, s);
-}
-
-// mode 1 / 0: run the one-row decode through the persistent step / the per-layer launches
-// (the captured step graph is dropped when that changes); -1: query.  available = the step's
-// stream is packed (TTS_STEP=1 at tts_lm_load on a TTS-1 geometry with 256 CUs).
-void lm_step_mode(Engine* e, int mode, int* available) {
-  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
-  TTS_REQUIRE(mode >= -1 && mode <= 2, "bad step mode");
-  TTS_REQUIRE(mode < 1 || e->w.step_ok, "the persistent step is not available for this model");
-  if (mode >= 0 && mode != e->w.step_mode) {
-    e->w.step_mode = mode;
-    if (e->w.graph) {
-      HIP_CHECK(hipStreamSynchronize(e->stream));
-      (void)hipGraphExecDestroy(e->w.graph);
-      e->w.graph = nullptr;
-      e->w.graph_batch = -1;
-    }
-  }
-  if (available) *available = e->w.step_ok ? 1 : 0;
-}
-
-// Diagnostics: one decode-step pass of the layer stack over one row (token embedding at
-// position pos of slot 0, the KV cache as it stands) through the persistent step (path 1)
-// or the per-layer launches (path 0); the row's residual stream after the last layer to
-// host fp32 [hidden].  The parity tests compare the two paths layer stack against layer
-// stack (tests/test_gpu_step.py).
-void lm_step_probe(Engine* e, int token, int pos, int path, float* x_out) {
-  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
-  TTS_REQUIRE(path >= 0 && path <= 5, "bad probe path");
-  TTS_REQUIRE(path == 0 || e->w.step_ok, "the persistent step is not available for this model");
-  TTS_REQUIRE(pos >= 0 && pos < e->lm.cfg.max_seq_len && token >= 0 && token < e->lm.cfg.vocab_size, "bad probe");
-  hipStream_t s = e->stream;
-  Ctx X(e, s);
-  const int HID = X.c.hidden_size;
-  const int zero = 0;
-  HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, &token, 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, &zero, 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(e->w.row_pos.p, &pos, 4, hipMemcpyHostToDevice, s));
-  launch_embed(e->w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), 1, HID, s);
-  if (path >= 2 && path <= 4) {  // the persistent step with its per-phase stamps: x_out = [layer][CU][kStepEvents] us
-                    // (path 3: every hand-off taken as ready, results garbage: the stream's own pace)
-    const size_t n = (size_t)X.c.num_layers * e->num_cu * kStepEvents;
-    unsigned long long* tr = nullptr;
-    HIP_CHECK(hipMalloc(&tr, n * 8));
-    HIP_CHECK(hipMemsetAsync(tr, 0, n * 8, s));
-    StepArgs sa = X.step_args(e->w.row_slot.as<int>(), e->w.row_pos.as<int>());
-    sa.trace = tr;
-    sa.nodeps = path - 2;
-    launch_decode_step(sa, s);
-    HIP_CHECK(hipGetLastError());
-    std::vector<unsigned long long> t(n);
-    HIP_CHECK(hipMemcpyAsync(t.data(), tr, n * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    HIP_CHECK(hipFree(tr));
-    unsigned long long t0 = ~0ull;
-    for (unsigned long long v : t)
-      if (v) t0 = std::min(t0, v);
-    for (size_t i = 0; i < n; ++i) x_out[i] = t[i] ? (float)(t[i] - t0) * 0.01f : -1.f;
-    check_fattn(e, s);
-    return;
-  }
-  const int saved = e->w.step_mode;
-  e->w.step_mode = path == 1 ? 1 : path == 5 ? 2 : 0;
-  X.layers(1, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
-  e->w.step_mode = saved;
-  HIP_CHECK(hipGetLastError());
-  // x_out: [hidden] residual stream, then the last layer's qkv [QKV] and attention output [H*D]
-  const int QKV = X.QKV(), HD = X.c.num_heads * X.c.head_dim;
-  std::vector<uint16_t> h(HID + QKV + HD);
-  HIP_CHECK(hipMemcpyAsync(h.data(), e->w.x.p, HID * 2, hipMemcpyDeviceToHost, s));
-  if (path == 0 || path == 5) {
-    HIP_CHECK(hipMemcpyAsync(h.data() + HID, e->w.qkv.p, QKV * 2, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(h.data() + HID + QKV, e->w.attn_out.p, HD * 2, hipMemcpyDeviceToHost, s));
-  } else {  // the step's granules of the last layer (lm_step.hip: G_QKV at HID/2, G_ATT after it)
-    std::vector<uint64_t> g((QKV + HD) / 2);
-    const uint64_t* gl = e->w.sgran.as<uint64_t>() + step_gran_elems(X.c.num_layers) / X.c.num_layers * (X.c.num_layers - 1);
-    HIP_CHECK(hipMemcpyAsync(g.data(), gl + HID / 2, g.size() * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    for (size_t i = 0; i < g.size(); ++i) {
-      h[HID + 2 * i] = (uint16_t)(g[i] & 0xffff);
-      h[HID + 2 * i + 1] = (uint16_t)((g[i] >> 16) & 0xffff);
-    }
-  }
-  HIP_CHECK(hipStreamSynchronize(s));
-  check_fattn(e, s);
-  for (size_t i = 0; i < h.size(); ++i) {
-    uint32_t u = (uint32_t)h[i] << 16;
-    memcpy(&x_out[i], &u, 4);
-  }
 }
 
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,

@@ -125,41 +125,6 @@ bool wgemm_supported(int M, int N, int K, int epi);
 bool wgemm_fattn_ok(int N, int K, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
 
-// ---- the one-row decode step's layers as one persistent launch (lm_step.hip; TTS-1 geometry)
-struct StepArgs {
-  static constexpr int kMaxLayers = 32;
-  const void* stream = nullptr;                 // weight stream: [slot][CU][16 KiB] (launch_step_pack)
-  const bf16_t* ln1 = nullptr;                  // layer 0's RMSNorm weights (input, post-attention);
-  const bf16_t* ln2 = nullptr;                  //   layer l's at + l * ln_stride elements
-  long long ln_stride = 0;
-  int L = 0;
-  float eps = 0.f, scale = 0.f;
-  bf16_t* x = nullptr;                          // row 0: the token embedding in, the last layer's output out
-  bf16_t* kv = nullptr;                         // KV cache (lm_attn.hip layout), layer stride 2 * kv_layer
-  long long kv_layer = 0;
-  int kv_stride = 0;
-  const int* row_slot = nullptr;                // the row's KV slot and position (device)
-  const int* row_pos = nullptr;
-  const bf16_t* rope_cos = nullptr;
-  const bf16_t* rope_sin = nullptr;
-  uint64_t* gran = nullptr;                     // hand-off granules (step_gran_elems)
-  int* seq = nullptr;                           // the step's tag (advanced by the kernel)
-  int* done = nullptr;                          // arrival counter (0 between steps)
-  int* err = nullptr;                           // set on a hand-off timeout
-  unsigned long long* trace = nullptr;          // diagnostics: [layer][CU][kStepEvents] s_memrealtime stamps
-  int nodeps = 0;                               // diagnostics: take every hand-off as ready (wrong
-                                                //   results; the weight stream's own pace)
-};
-constexpr int kStepEvents = 16;
-bool step_supported(int hidden, int heads, int kv_heads, int head_dim, int ffn, int layers, int num_cu);
-size_t step_stream_bytes(int layers);
-size_t step_gran_elems(int layers);
-void launch_decode_step(const StepArgs& a, hipStream_t s);
-// the MLP half of layer `layer` for one row (h in a.x -> x over it) on the same stream
-void launch_mlp_block(const StepArgs& a, int layer, hipStream_t s);
-// row-major W of one layer's matrix -> the step's weight stream; kind 0 qkv, 1 o, 2 gate, 3 up, 4 down
-void launch_step_pack(const bf16_t* w, void* stream, int kind, int layer, int L, hipStream_t s);
-
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
 // MFMA blocks; epilogues EPI_STORE / EPI_RESID / EPI_SWIGLU; no fused RMSNorm
 struct PgemmArgs {

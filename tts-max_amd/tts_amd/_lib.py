@@ -46,8 +46,6 @@ EXPORTED_SYMBOLS = (
     "tts_lm_id_to_code",
     "tts_lm_last_timing",
     "tts_lm_bench_kernel",
-    "tts_lm_step_mode",
-    "tts_lm_step_probe",
     "tts_codec_load",
     "tts_codec_decode",
     "tts_codec_samples_per_code",
@@ -170,8 +168,6 @@ def load_library() -> ctypes.CDLL:
         "tts_lm_id_to_code": (I32, [P, pi32, I32, pi32]),
         "tts_lm_last_timing": (I32, [P, ctypes.POINTER(F32), ctypes.POINTER(F32), pi32]),
         "tts_lm_bench_kernel": (I32, [P, I32, I32, I32, I32, ctypes.POINTER(F32), ctypes.POINTER(ctypes.c_double)]),
-        "tts_lm_step_mode": (I32, [P, I32, pi32]),
-        "tts_lm_step_probe": (I32, [P, I32, I32, I32, ctypes.POINTER(F32)]),
         "tts_codec_load": (I32, [P, ctypes.POINTER(CodecConfig), ctypes.POINTER(TensorDesc), I32]),
         "tts_codec_decode": (I32, [P, pi32, pi32, I32, P, I32, ctypes.POINTER(ctypes.c_int64), P]),
         "tts_codec_samples_per_code": (I32, [P, pi32]),

@@ -331,25 +331,12 @@ class MI355XSpeechLM:
     def bench_kernel(self, which: str, rows: int = 1, ctx: int = 450, iters: int = 50) -> tuple[float, float]:
         """(avg ms per launch, algorithmic bytes per launch) of one decode-step kernel."""
         ms, b = ctypes.c_float(), ctypes.c_double()
-        # qkv_attn: QKV with the decode attention fused in (the launch path's one-row form);
-        # step: every layer of the one-row step as the persistent launch (lm_step.hip);
-        # mlp: one layer's gate/up + down as one launch on that engine
-        sel = {"qkv_attn": 6, "step": 7, "mlp": 8}.get(which)
+        # qkv_attn: QKV with the decode attention fused in (the one-row step's form)
+        sel = {"qkv_attn": 6}.get(which)
         sel = self.KERNELS.index(which) if sel is None else sel
         _lib.check(self._lib.tts_lm_bench_kernel(self._h, sel, rows, ctx, iters,
                                                  ctypes.byref(ms), ctypes.byref(b)))
         return ms.value, b.value
-
-    def step_available(self) -> bool:
-        """Whether the persistent one-row step (lm_step.hip) was packed at load (TTS_STEP=1)."""
-        av = ctypes.c_int32()
-        _lib.check(self._lib.tts_lm_step_mode(self._h, -1, ctypes.byref(av)))
-        return bool(av.value)
-
-    def set_step(self, mode) -> None:
-        """One-row decode path: 1 / True = the persistent step, 2 = per-layer launches with the
-        MLP half as one launch on the step engine, 0 / False = the per-layer launches."""
-        _lib.check(self._lib.tts_lm_step_mode(self._h, int(mode), None))
 
     def ids_to_codes(self, ids: Sequence[int]) -> list[int]:
         arr = np.ascontiguousarray(np.asarray(ids, dtype=np.int32))
