@@ -507,6 +507,11 @@ static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, 
   HIP_CHECK(hipMemcpyAsync(X.w.row_idx.p, tok.data(), rows * 4, hipMemcpyHostToDevice, X.s));
   launch_embed(X.w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), X.w.x.as<bf16_t>(), rows,
                X.c.hidden_size, X.s);
+  // the fused QKV + attention launch tags its granules (position, layer): a sequence starting
+  // over at a position an earlier sequence reached must not find that sequence's granules
+  // (with a matching tag the attention workgroups could read them before this step's QKV
+  // workgroups overwrite them)
+  HIP_CHECK(hipMemsetAsync(X.w.gran.p, 0xff, X.w.gran.bytes, X.s));
 }
 
 // The decode step (all layers + lm_head + pick + finalize over B rows) captured once into a
