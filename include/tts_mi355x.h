@@ -226,6 +226,30 @@ tts_status tts_codec_decode(tts_engine* e, const int32_t* codes, const int32_t* 
 
 tts_status tts_codec_samples_per_code(tts_engine* e, int32_t* out);
 
+/* --------------------------------------------------------- prompt-audio encoder ---- */
+
+/* Loads the codec ENCODER (the reference `Encoder` minus its w2v-bert feature model,
+ * tts/core/codec/encoder.py:20-46): host f32 tensors by the reference state-dict names —
+ * "semantic_encoder.*", "acoustic_encoder.*" (legacy weight_norm weight_g / weight_v; folded
+ * here), "fusion_layer.*", "quantizer.project_in.*", and the anti-aliasing filter buffers
+ * "acoustic_encoder.conv_final_block.0.upsample.filter" /
+ * "...downsample.lowpass.filter" ([1, 1, 12]).  Replaces encoding.create / Encoder.__init__
+ * + load_from_checkpoint (encoding.py:75-80, encoder.py:20-113). */
+tts_status tts_encoder_load(tts_engine* e, const tts_tensor_desc* t, int32_t n);
+
+/* Encodes one 16 kHz waveform to codec codes — Encoder.encode (encoder.py:115-128) from the
+ * padding on, in fp32 on the device:
+ *   wav           host f32 [n_samples]
+ *   w2v_features  host f32 [n_frames][1024]: w2v-bert-2.0 hidden_states[16] of the padded
+ *                 waveform's SeamlessM4T features (the reference's wav2vec_model call,
+ *                 encoder.py:71; computed by the caller), n_frames = the 320-sample hops of
+ *                 the waveform padded to a whole hop (plus one hop when already whole)
+ *   codes         host int32 [codes_cap] <- n_codes = n_frames FSQ indices
+ *   pre_round     optional host f32 [n_frames][8]: the values the FSQ rounded (diagnostics) */
+tts_status tts_encoder_encode(tts_engine* e, const float* wav, int64_t n_samples, const float* w2v_features,
+                              int32_t n_frames, int32_t* codes, int32_t codes_cap, int32_t* n_codes,
+                              float* pre_round);
+
 #ifdef __cplusplus
 }
 #endif

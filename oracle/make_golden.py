@@ -405,6 +405,100 @@ def codec_fixture(name: str, manifest: dict) -> None:
     print(name, json.dumps(stats))
 
 
+# The prompt-audio encoder (§8f rank 1): the reference's own Encoder.encode
+# (tts/core/codec/encoder.py:115-128) on synthetic weights.  Its __init__ loads the
+# feature extractor and w2v-bert-2.0 from the hub, so the object is assembled here with the
+# same modules (encoder.py:20-56) and transformers' SeamlessM4TFeatureExtractor /
+# Wav2Vec2BertModel from a local config (configs.EncoderArch: the hub dimensions, parity of
+# those dimensions unpinned).  (seed, [(wav seed, samples)])
+ENCODER_CASES = {"encoder_16k": (0xE2C0, [(0, 8000), (1, 20800), (2, 48123)])}
+
+
+def build_reference_encoder(arch, seed):
+    """The reference Encoder object with synthetic weights (no hub access)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "shims"))
+    sys.path.insert(0, "/root/reference")
+    import transformers
+    import vector_quantize_pytorch as vq  # the shim (vector_quantize_pytorch 1.17.8 restated)
+    from tts.core.codec import encoder as ref_encoder, encoder_modules  # the reference's own code
+
+    enc = ref_encoder.Encoder.__new__(ref_encoder.Encoder)
+    torch.nn.Module.__init__(enc)
+    enc.sample_rate, enc.token_rate = arch.sample_rate, arch.token_rate
+    enc.semantic_encoder = encoder_modules.SemanticEncoder(input_channels=1024, output_channels=1024,
+                                                           encode_channels=1024, kernel_size=3)
+    enc.acoustic_encoder = encoder_modules.AcousticEncoder(
+        num_generator_features=arch.ngf, initial_conv_kernel_size=7, final_conv_kernel_size=3,
+        up_ratios=list(arch.up_ratios), dilations=tuple(arch.dilations), output_dim=arch.acoustic_dim)
+    enc.fusion_layer = torch.nn.Linear(2048, 2048)
+    enc.quantizer = vq.ResidualFSQ(dim=2048, levels=list(arch.levels), num_quantizers=1)
+    w = synth.weights_from_specs_cpu(synth.encoder_tensor_specs(arch), seed)
+    missing, unexpected = enc.load_state_dict(w, strict=False)
+    assert not unexpected, unexpected
+    assert all(m.endswith("filter") for m in missing), missing  # the anti-aliasing buffers
+    enc.wav2vec_feature_extractor = transformers.SeamlessM4TFeatureExtractor(padding_value=1.0)
+    cfg = transformers.Wav2Vec2BertConfig(**arch.w2v_hf_config())
+    enc.wav2vec_model = transformers.Wav2Vec2BertModel(cfg)
+    enc.wav2vec_model.config.output_hidden_states = True
+    enc.wav2vec_model.load_state_dict(synth.weights_from_specs_cpu(synth.w2v_tensor_specs(arch), seed + 1),
+                                      strict=True)
+    enc.eval()
+    return enc
+
+
+def encoder_fixture(name: str, manifest: dict) -> None:
+    arch = configs.ENCODER
+    seed, cases = ENCODER_CASES[name]
+    t0 = time.time()
+    enc = build_reference_encoder(arch, seed)
+    filt = enc.acoustic_encoder.conv_final_block[0]
+    up_f, dn_f = filt.upsample.filter.flatten(), filt.downsample.lowpass.filter.flatten()
+    assert torch.equal(up_f, synth.kaiser_sinc_filter(0.25, 0.3, 12))
+    assert torch.equal(dn_f, synth.kaiser_sinc_filter(0.25, 0.3, 12))
+    rec = dict(wav=[], wav_lens=[], feats=[], w2v=[], acoustic=[], pre_round=[], codes=[], T=[])
+    stats = []
+    hooks = {}
+    enc.acoustic_encoder.register_forward_hook(lambda m, i, o: hooks.__setitem__("acoustic", o.detach()))
+    enc.quantizer.layers[0].register_forward_hook(lambda m, i, o: hooks.__setitem__("fsq_in", i[0].detach()))
+    for ws, n in cases:
+        wav = torch.from_numpy(synth.synthetic_wav(ws, n))[None]
+        with torch.no_grad():
+            codes = enc.encode(wav)  # the reference call (encoding.py:67-72 -> encoder.py:115-128)
+            # the intermediate tensors of the same call, recomputed for the fixture
+            audio = torch.nn.functional.pad(wav, (0, 320 - (wav.shape[1] % 320)))
+            audio_pad = torch.nn.functional.pad(audio, (160, 160))
+            feat = enc.wav2vec_feature_extractor(audio_pad, sampling_rate=16000,
+                                                 return_tensors="pt").data["input_features"]
+            w2v = enc.wav2vec_model(feat).hidden_states[16]
+        codes = codes.reshape(-1).numpy().astype(np.int32)
+        T = codes.size
+        fsq_in = hooks["fsq_in"].reshape(T, -1).float()  # the FSQ layer's input = bound(project_in(x))
+        lv = torch.tensor(arch.levels, dtype=torch.float32)
+        pre = enc.quantizer.layers[0].bound(fsq_in)  # the value torch.round sees
+        stats.append(dict(samples=n, T=int(T), feats=list(feat.shape), w2v_rms=float(w2v.pow(2).mean().sqrt()),
+                          acoustic_rms=float(hooks["acoustic"].pow(2).mean().sqrt()),
+                          min_round_margin=float((pre - pre.round()).abs().sub(0.5).abs().min()),
+                          distinct_codes=int(len(set(codes.tolist())))))
+        rec["wav"].append(wav[0].numpy())
+        rec["wav_lens"].append(n)
+        rec["feats"].append(feat[0].numpy().astype(np.float32))
+        rec["w2v"].append(w2v[0].numpy().astype(np.float32))
+        rec["acoustic"].append(hooks["acoustic"][0].numpy().astype(np.float32))
+        rec["pre_round"].append(pre.numpy().astype(np.float32))
+        rec["codes"].append(codes)
+        rec["T"].append(int(T))
+        print(name, json.dumps(stats[-1]), flush=True)
+        del lv
+    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), seed=seed,
+                        **{k: (np.concatenate(v) if k not in ("wav_lens", "T") else np.asarray(v))
+                           for k, v in rec.items()})
+    manifest[name] = dict(kind="encoder", arch=arch.name, seed=seed,
+                          generator="reference tts.core.codec.encoder.Encoder.encode (fp32, CPU) + oracle/shims; "
+                          f"transformers {__import__('transformers').__version__} SeamlessM4TFeatureExtractor / "
+                          "Wav2Vec2BertModel from a local config (w2v-bert-2.0 dims: parity unpinned)",
+                          cases=stats, seconds=round(time.time() - t0, 1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*")
@@ -414,10 +508,11 @@ def main():
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     torch.manual_seed(0)
     names = args.only or (list(LM_CASES) + list(CHAIN_CASES) + list(SYNTH_CASES) + list(CONFIG1_CASES) +
-                          list(CODEC_CASES))
+                          list(CODEC_CASES) + list(ENCODER_CASES))
     for n in names:
         fn = (lm_fixture if n in LM_CASES else chain_fixture if n in CHAIN_CASES else
-              synth_fixture if n in SYNTH_CASES else config1_fixture if n in CONFIG1_CASES else codec_fixture)
+              synth_fixture if n in SYNTH_CASES else config1_fixture if n in CONFIG1_CASES else
+              encoder_fixture if n in ENCODER_CASES else codec_fixture)
         fn(n, manifest)
         with open(mpath, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)

@@ -46,3 +46,46 @@ class ResidualFSQ(torch.nn.Module):
     def get_output_from_indices(self, indices):
         codes = self.get_codes_from_indices(indices)
         return self.project_out(codes.sum(0))
+
+
+# ---- the quantize (encoder) direction, vector_quantize_pytorch 1.17.8 inference path ----
+# FSQ.bound: half_l = (L - 1)(1 + eps) / 2, offset = 0.5 for even L, shift = atanh(offset /
+# half_l), bounded = tanh(z + shift) * half_l - offset; quantize = round(bound(z)) / (L // 2);
+# codes_to_indices: sum((codes * (L // 2) + L // 2) * basis).  ResidualFSQ.forward bounds the
+# projected input once with the first quantizer's bound before the per-quantizer loop, whose
+# FSQ bounds again (the HF Xcodec2 port keeps both for checkpoint consistency).
+
+
+def _fsq_bound(self, z, eps=1e-3):
+    levels = self._levels.to(z.dtype)
+    half_l = (levels - 1) * (1 + eps) / 2
+    offset = torch.where(self._levels % 2 == 0, 0.5, 0.0).to(z.dtype)
+    shift = (offset / half_l).atanh()
+    return (z + shift).tanh() * half_l - offset
+
+
+def _fsq_forward(self, z):
+    z = z.float()
+    half_width = (self._levels // 2).to(z.dtype)
+    codes = self.bound(z).round() / half_width
+    indices = ((codes * half_width + half_width) * self._basis.to(z.dtype)).sum(dim=-1).to(torch.int32)
+    return codes, indices
+
+
+def _rfsq_forward(self, x):
+    x = self.project_in(x)
+    residual = self.layers[0].bound(x)
+    quantized_out = 0.0
+    all_indices = []
+    for layer, scale in zip(self.layers, self.scales):
+        quantized, indices = layer(residual / scale)
+        quantized = quantized * scale
+        residual = residual - quantized.detach()
+        quantized_out = quantized_out + quantized
+        all_indices.append(indices)
+    return self.project_out(quantized_out), torch.stack(all_indices, dim=-1)
+
+
+FSQ.bound = _fsq_bound
+FSQ.forward = _fsq_forward
+ResidualFSQ.forward = _rfsq_forward

@@ -56,6 +56,9 @@ def test_manifest_records_oracle_agreement():
                 assert c["hf_min_margin"] >= 4 * max(c["top2_dev_vs_oracle_max"], 1.0), (name, c)
             elif m["kind"] == "codec":
                 assert c["oracle_rel_l2"] < 1e-4, (name, c)
+            elif m["kind"] == "encoder":
+                # decisive codes: every rounded value far from a rounding boundary
+                assert c["min_round_margin"] > 0.01 and c["distinct_codes"] > 1, (name, c)
 
 
 @pytest.mark.parametrize("name", ["codec_24k_d2", "codec_16k"])
@@ -134,3 +137,24 @@ def test_sample_probs_match_transformers_warpers(T, k, p):
         ref = torch.softmax(warpers(None, s.clone()), dim=-1)[0]
         got = lm_oracle.sample_probs(s[0], T, k, p)
         assert torch.allclose(got, ref, atol=1e-7, rtol=0), (got - ref).abs().max()
+
+
+def test_encoder_oracle_reproduces_reference():
+    """oracle/encoder_oracle.py (a functional restatement of the reference Encoder after
+    w2v-bert) reproduces the reference's codes on the fixture's waveforms and features."""
+    from tts_amd import configs, synth
+    from oracle import encoder_oracle
+
+    z = np.load(os.path.join(GOLDEN, "encoder_16k.npz"))
+    w = synth.weights_from_specs_cpu(synth.encoder_tensor_specs(configs.ENCODER), int(z["seed"]))
+    filt = synth.kaiser_sinc_filter(0.25, 0.3, 12)
+    wo = to = 0
+    for n, T in zip(z["wav_lens"], z["T"]):
+        n, T = int(n), int(T)
+        with torch.no_grad():
+            codes, pre = encoder_oracle.encode(w, torch.from_numpy(z["wav"][wo:wo + n]),
+                                               torch.from_numpy(z["w2v"][to:to + T]), filt)
+        np.testing.assert_array_equal(codes.numpy(), z["codes"][to:to + T])
+        assert np.abs(pre.numpy() - z["pre_round"][to:to + T]).max() < 5e-3
+        wo += n
+        to += T

@@ -38,6 +38,7 @@ Engine::~Engine() {
   if (w.graph) (void)hipGraphExecDestroy(w.graph);
   if (w.h_active) (void)hipHostFree(w.h_active);
   if (codec) codec_destroy(codec);
+  if (encoder) encoder_destroy(encoder);
   for (auto& v : ev)
     if (v) (void)hipEventDestroy(v);
   if (stream) (void)hipStreamDestroy(stream);
@@ -246,6 +247,27 @@ tts_status tts_codec_decode(tts_engine* e, const int32_t* codes, const int32_t* 
     Engine* E = reinterpret_cast<Engine*>(e);
     HIP_CHECK(hipSetDevice(E->device));
     codec_decode(E, codes, lens, batch, wav, wav_is_device, wav_lens, pick_stream(E, stream));
+  });
+}
+
+tts_status tts_encoder_load(tts_engine* e, const tts_tensor_desc* t, int32_t n) {
+  return guarded([&] {
+    TTS_REQUIRE(e && t && n > 0, "null argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    encoder_load(E, t, n);
+  });
+}
+
+tts_status tts_encoder_encode(tts_engine* e, const float* wav, int64_t n_samples, const float* w2v_features,
+                              int32_t n_frames, int32_t* codes, int32_t codes_cap, int32_t* n_codes,
+                              float* pre_round) {
+  return guarded([&] {
+    TTS_REQUIRE(e && wav && w2v_features && codes && n_codes, "null argument");
+    TTS_REQUIRE(n_samples >= 1 && n_samples < (1ll << 31) - 640, "bad waveform length");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    *n_codes = encoder_encode(E, wav, (int)n_samples, w2v_features, n_frames, codes, codes_cap, pre_round);
   });
 }
 

@@ -108,7 +108,8 @@ struct LmWork {
   int* h_active = nullptr;  // pinned host copy of n_active (ring of 2)
 };
 
-struct Codec;  // codec_engine.cpp
+struct Codec;         // codec_engine.cpp
+struct AudioEncoder;  // codec_encoder.cpp
 
 struct Engine {
   int device = 0;
@@ -118,6 +119,7 @@ struct Engine {
   LmModel lm;
   LmWork w;
   Codec* codec = nullptr;
+  AudioEncoder* encoder = nullptr;
   float t_prefill_ms = 0.f, t_decode_ms = 0.f;
   int decode_steps = 0;
   // an open generation (tts_generate_begin .. tts_generate_read): state lives on the device
@@ -169,6 +171,11 @@ void codec_load(Engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t
 void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, float* wav,
                   int wav_is_device, int64_t* wav_lens, hipStream_t s);
 int codec_samples_per_code(Engine* e);
+// the prompt-audio encoder (codec_encoder.cpp)
+void encoder_load(Engine* e, const tts_tensor_desc* t, int n);
+int encoder_encode(Engine* e, const float* wav, int n, const float* w2v, int T_w2v, int32_t* codes, int cap,
+                   float* pre);
+void encoder_destroy(AudioEncoder* a);
 void codec_destroy(Codec* c);
 
 }  // namespace tts

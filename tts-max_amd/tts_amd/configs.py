@@ -152,6 +152,49 @@ CODEC_ARCHS = {a.name: a for a in (CODEC_16K, CODEC_24K, CODEC_48K, CODEC_24K_D2
 
 
 @dataclasses.dataclass(frozen=True)
+class EncoderArch:
+    """The prompt-audio codec encoder (tts/core/codec/encoder.py:20-56): SemanticEncoder over
+    w2v-bert-2.0 layer-16 features, AcousticEncoder over the 16 kHz waveform, fusion Linear,
+    ResidualFSQ (one quantizer, 8 levels of 4).  The w2v-bert dimensions are the hub model's
+    (facebook/w2v-bert-2.0, not in the reference tree): parity of those dimensions is
+    unpinned; the arithmetic is transformers' Wav2Vec2BertModel."""
+
+    name: str = "encoder-16k"
+    sample_rate: int = 16000
+    token_rate: int = 50
+    hop: int = 320
+    ngf: int = 48                                   # AcousticEncoder num_generator_features
+    up_ratios: tuple[int, ...] = (2, 2, 4, 4, 5)
+    dilations: tuple[int, ...] = (1, 3, 9)
+    acoustic_dim: int = 1024
+    semantic_dim: int = 1024
+    levels: tuple[int, ...] = (4, 4, 4, 4, 4, 4, 4, 4)
+    # w2v-bert-2.0 (hub config): only the first `w2v_layers` layers feed hidden_states[16]
+    w2v_hidden: int = 1024
+    w2v_layers: int = 16
+    w2v_heads: int = 16
+    w2v_ffn: int = 4096
+    w2v_feat_in: int = 160
+    w2v_left: int = 64
+    w2v_right: int = 8
+    w2v_conv_k: int = 31
+    w2v_eps: float = 1e-5
+
+    def w2v_hf_config(self) -> dict:
+        return dict(hidden_size=self.w2v_hidden, num_hidden_layers=self.w2v_layers,
+                    num_attention_heads=self.w2v_heads, intermediate_size=self.w2v_ffn,
+                    feature_projection_input_dim=self.w2v_feat_in, hidden_act="swish",
+                    position_embeddings_type="relative_key", left_max_position_embeddings=self.w2v_left,
+                    right_max_position_embeddings=self.w2v_right, conv_depthwise_kernel_size=self.w2v_conv_k,
+                    layer_norm_eps=self.w2v_eps, add_adapter=False, hidden_dropout=0.0,
+                    attention_dropout=0.0, activation_dropout=0.0, feat_proj_dropout=0.0,
+                    conformer_conv_dropout=0.0, layerdrop=0.0, apply_spec_augment=False)
+
+
+ENCODER = EncoderArch()
+
+
+@dataclasses.dataclass(frozen=True)
 class SpeechVocab:
     """Token-id layout produced by tts/core/tokenization.py:36-61: the 8 control tokens and
     the 65,536 ``<|s_N|>`` tokens are added in ``sorted()`` (lexicographic) order after the

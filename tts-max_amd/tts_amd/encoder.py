@@ -1,0 +1,156 @@
+"""Prompt-audio encoder surface backed by the MI355X engine.
+
+Drop-in for tts/core/codec/encoding.py: ``AudioEncoderInterface`` (9-26), ``AudioEncoder``
+(29-52: encode(wav [1, N] at 16 kHz) -> codes, sample_rate, token_rate),
+``CachingAudioEncoder`` (55-72: per-prompt-id cache, codes as a list) and ``create`` (75-80).
+
+Split of the work (the reference runs it all in ``Encoder.encode``, encoder.py:115-128):
+
+* host (CPU, as the reference): the padding and transformers' SeamlessM4TFeatureExtractor;
+* w2v-bert-2.0 up to hidden_states[16] (the reference's ``wav2vec_model``): transformers'
+  Wav2Vec2BertModel on the same GPU through PyTorch — the one part of the encoder not yet a
+  HIP kernel;
+* everything after it — AcousticEncoder over the waveform (Snake with the anti-aliased
+  2x filters, dilated and strided convolutions), SemanticEncoder, fusion, ResidualFSQ
+  quantisation — in fp32 HIP kernels through ``tts_encoder_encode``.
+"""
+
+from __future__ import annotations
+
+import abc
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, configs, synth
+
+
+class AudioEncoderInterface(metaclass=abc.ABCMeta):
+    """Same abstract surface as tts.core.codec.encoding.AudioEncoderInterface."""
+
+    @abc.abstractmethod
+    def encode(self, wav: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    @property
+    @abc.abstractmethod
+    def sample_rate(self) -> int:
+        raise NotImplementedError
+
+    @property
+    @abc.abstractmethod
+    def token_rate(self) -> int:
+        raise NotImplementedError
+
+
+def pad_like_reference(wav: torch.Tensor, hop: int = 320) -> tuple[torch.Tensor, torch.Tensor]:
+    """encoder.py:117-120: pad to a whole hop (a full extra hop when already whole, as the
+    reference's ``hop - n % hop`` does), then half a hop each side for the feature extractor."""
+    audio = torch.nn.functional.pad(wav.cpu().float(), (0, hop - (wav.shape[-1] % hop)))
+    return audio, torch.nn.functional.pad(audio, (hop // 2, hop // 2))
+
+
+class MI355XAudioEncoder(AudioEncoderInterface):
+    """One encoder resident on one MI355X (its own engine)."""
+
+    def __init__(self, weights: dict[str, torch.Tensor], w2v_model: torch.nn.Module, feature_extractor,
+                 arch: configs.EncoderArch = configs.ENCODER, device: int = 0):
+        self.arch = arch
+        self.device = torch.device("cuda", device)
+        self._lib = _lib.load_library()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.tts_engine_create(device, ctypes.byref(h)))
+        self._h = h
+        tensors = {k: v.detach().float().cpu().contiguous() for k, v in weights.items()}
+        descs, keep = _lib.make_descs(tensors)
+        _lib.check(self._lib.tts_encoder_load(self._h, descs, len(tensors)))
+        del keep
+        self._w2v = w2v_model.to(self.device).eval()
+        self._fe = feature_extractor
+
+    @classmethod
+    def synthetic(cls, arch: configs.EncoderArch = configs.ENCODER, seed: int = 0xE2C0, device: int = 0):
+        """Random-init weights of the encoder (synth.encoder_tensor_specs, seed) and of the
+        w2v-bert model (synth.w2v_tensor_specs, seed + 1) — the generator the golden fixture
+        tests/golden/encoder_16k.npz was made with."""
+        import transformers
+
+        w = synth.weights_from_specs_cpu(synth.encoder_tensor_specs(arch), seed)
+        f = synth.kaiser_sinc_filter(0.25, 0.3, 12).view(1, 1, 12)
+        w["acoustic_encoder.conv_final_block.0.upsample.filter"] = f
+        w["acoustic_encoder.conv_final_block.0.downsample.lowpass.filter"] = f.clone()
+        cfg = transformers.Wav2Vec2BertConfig(**arch.w2v_hf_config())
+        with torch.device("meta"):
+            w2v = transformers.Wav2Vec2BertModel(cfg)
+        w2v = w2v.to_empty(device="cpu")
+        w2v.load_state_dict(synth.weights_from_specs_cpu(synth.w2v_tensor_specs(arch), seed + 1), strict=True)
+        fe = transformers.SeamlessM4TFeatureExtractor(padding_value=1.0)
+        return cls(w, w2v, fe, arch=arch, device=device)
+
+    @property
+    def sample_rate(self) -> int:
+        return self.arch.sample_rate
+
+    @property
+    def token_rate(self) -> int:
+        return self.arch.token_rate
+
+    @torch.no_grad()
+    def w2v_features(self, wav: torch.Tensor) -> np.ndarray:
+        """w2v-bert-2.0 hidden_states[16] of the reference-padded waveform [1, N] -> [T, 1024]."""
+        _, audio_pad = pad_like_reference(wav.reshape(1, -1), self.arch.hop)
+        feat = self._fe(audio_pad, sampling_rate=self.arch.sample_rate, return_tensors="pt").data["input_features"]
+        out = self._w2v(feat.to(self.device), output_hidden_states=True).hidden_states[16]
+        return np.ascontiguousarray(out[0].float().cpu().numpy())
+
+    def encode_with_features(self, wav: np.ndarray, w2v: np.ndarray, return_pre: bool = False):
+        """The HIP part of Encoder.encode: waveform [N] + its w2v-bert features [T, 1024] ->
+        codes [T] (and the values the FSQ rounded, [T, 8])."""
+        wav = np.ascontiguousarray(wav, dtype=np.float32).reshape(-1)
+        w2v = np.ascontiguousarray(w2v, dtype=np.float32)
+        T = w2v.shape[0]
+        codes = np.zeros(T, dtype=np.int32)
+        pre = np.zeros((T, len(self.arch.levels)), dtype=np.float32) if return_pre else None
+        n = ctypes.c_int32()
+        f32p = ctypes.POINTER(ctypes.c_float)
+        _lib.check(self._lib.tts_encoder_encode(
+            self._h, wav.ctypes.data_as(f32p), wav.size, w2v.ctypes.data_as(f32p), T,
+            codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), T, ctypes.byref(n),
+            pre.ctypes.data_as(f32p) if return_pre else None))
+        return (codes[: n.value], pre) if return_pre else codes[: n.value]
+
+    @torch.no_grad()
+    def encode(self, wav: torch.Tensor) -> torch.Tensor:
+        """AudioEncoder.encode (encoding.py:42-45 -> encoder.py:115-128): wav [1, N] at
+        16 kHz -> codes [T] (int64, CPU; the reference's .squeeze() of the [1, 1, T] codes)."""
+        wav = wav.reshape(1, -1)
+        codes = self.encode_with_features(wav[0].float().cpu().numpy(), self.w2v_features(wav))
+        return torch.from_numpy(codes.astype(np.int64))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.tts_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class CachingAudioEncoder:
+    """encoding.py:55-72: encodes a prompt once per prompt id; codes as a Python list."""
+
+    def __init__(self, encoder: AudioEncoderInterface):
+        self._encoder = encoder
+        self._prompt_encoding_cache: dict[str, list[int]] = {}
+
+    @torch.no_grad()
+    def encode(self, prompt_id: str, prompt_wav: torch.Tensor) -> list[int]:
+        if prompt_id in self._prompt_encoding_cache:
+            return self._prompt_encoding_cache[prompt_id]
+        codes = self._encoder.encode(prompt_wav).cpu().tolist()
+        self._prompt_encoding_cache[prompt_id] = codes
+        return codes

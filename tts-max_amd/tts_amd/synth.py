@@ -231,6 +231,131 @@ def chain_prompt(vocab, spec: ChainSpec, utt: int, start: int, n_text_tokens: in
     return base + toks[start - spec.lag - 1: start + 1]
 
 
+# -------------------------------------------------------------------- encoder weights ---
+
+def encoder_tensor_specs(cfg: configs.EncoderArch) -> list[tuple[str, tuple[int, ...], float, float]]:
+    """(name, shape, scale, offset) for the reference Encoder's own modules (encoder.py:20-46:
+    semantic_encoder, acoustic_encoder with legacy weight_norm g / v, fusion_layer,
+    quantizer.project_in / project_out).  Weight-norm directions v are uniform, magnitudes g
+    near 1 (a conv keeps its input's scale), SnakeBeta log-scale alpha / beta near 0."""
+    specs = []
+
+    def wn(pre, co, ci, k):
+        specs.extend([(pre + "weight_g", (co, 1, 1), 0.2, 1.0), (pre + "weight_v", (co, ci, k), 1.0, 0.0),
+                      (pre + "bias", (co,), 0.01, 0.0)])
+
+    def snake(pre, c):
+        specs.extend([(pre + "act.alpha", (c,), 0.3, 0.0), (pre + "act.beta", (c,), 0.3, 0.0)])
+
+    a = "acoustic_encoder."
+    d = cfg.ngf
+    wn(a + "conv_blocks.0.", d, 1, 7)
+    for i, stride in enumerate(cfg.up_ratios, start=1):
+        half, d = d, d * 2
+        for r, _ in enumerate(cfg.dilations):
+            pre = f"{a}conv_blocks.{i}.block.{r}.block."
+            snake(pre + "0.", half)
+            wn(pre + "1.", half, half, 7)
+            snake(pre + "2.", half)
+            wn(pre + "3.", half, half, 1)
+        snake(f"{a}conv_blocks.{i}.block.3.", half)
+        wn(f"{a}conv_blocks.{i}.block.4.", d, half, 2 * stride)
+    snake(a + "conv_final_block.0.", d)
+    wn(a + "conv_final_block.1.", cfg.acoustic_dim, d, 3)
+    S = cfg.semantic_dim
+    sc = math.sqrt(3.0 / (3 * S))
+    specs += [("semantic_encoder.initial_conv.weight", (S, S, 3), sc, 0.0),
+              ("semantic_encoder.residual_blocks.1.weight", (S, S, 3), sc, 0.0),
+              ("semantic_encoder.residual_blocks.1.bias", (S,), 0.01, 0.0),
+              ("semantic_encoder.residual_blocks.3.weight", (S, S, 3), sc, 0.0),
+              ("semantic_encoder.residual_blocks.3.bias", (S,), 0.01, 0.0),
+              ("semantic_encoder.final_conv.weight", (S, S, 3), sc, 0.0)]
+    F = S + cfg.acoustic_dim
+    fs = math.sqrt(3.0 / F)
+    specs += [("fusion_layer.weight", (F, F), fs, 0.0), ("fusion_layer.bias", (F,), 0.01, 0.0),
+              ("quantizer.project_in.weight", (len(cfg.levels), F), 2 * fs, 0.0),
+              ("quantizer.project_in.bias", (len(cfg.levels),), 0.1, 0.0),
+              ("quantizer.project_out.weight", (F, len(cfg.levels)), 0.2, 0.0),
+              ("quantizer.project_out.bias", (F,), 0.01, 0.0)]
+    return specs
+
+
+def w2v_tensor_specs(cfg: configs.EncoderArch) -> list[tuple[str, tuple[int, ...], float, float]]:
+    """(name, shape, scale, offset) for transformers' Wav2Vec2BertModel with
+    `cfg.w2v_hf_config()` (the names of its state dict; layer norms near 1, linear weights of
+    std 0.02 like its initializer)."""
+    H, FF, Fi, hd = cfg.w2v_hidden, cfg.w2v_ffn, cfg.w2v_feat_in, cfg.w2v_hidden // cfg.w2v_heads
+    lin = 0.02 * math.sqrt(3.0)
+
+    def ln(pre, n):
+        return [(pre + "weight", (n,), 0.1, 1.0), (pre + "bias", (n,), 0.02, 0.0)]
+
+    specs = [("masked_spec_embed", (H,), 0.1, 0.0)]
+    specs += ln("feature_projection.layer_norm.", Fi)
+    specs += [("feature_projection.projection.weight", (H, Fi), math.sqrt(3.0 / Fi), 0.0),
+              ("feature_projection.projection.bias", (H,), 0.01, 0.0)]
+    for i in range(cfg.w2v_layers):
+        p = f"encoder.layers.{i}."
+        for f in ("ffn1", "ffn2"):
+            specs += ln(p + f + "_layer_norm.", H)
+            specs += [(p + f + ".intermediate_dense.weight", (FF, H), lin, 0.0),
+                      (p + f + ".intermediate_dense.bias", (FF,), 0.01, 0.0),
+                      (p + f + ".output_dense.weight", (H, FF), lin, 0.0),
+                      (p + f + ".output_dense.bias", (H,), 0.01, 0.0)]
+        specs += ln(p + "self_attn_layer_norm.", H)
+        for n in ("q", "k", "v", "out"):
+            specs += [(p + f"self_attn.linear_{n}.weight", (H, H), lin, 0.0),
+                      (p + f"self_attn.linear_{n}.bias", (H,), 0.01, 0.0)]
+        specs.append((p + "self_attn.distance_embedding.weight", (cfg.w2v_left + cfg.w2v_right + 1, hd), 0.5, 0.0))
+        specs += ln(p + "conv_module.layer_norm.", H)
+        specs += [(p + "conv_module.pointwise_conv1.weight", (2 * H, H, 1), lin, 0.0),
+                  (p + "conv_module.depthwise_conv.weight", (H, 1, cfg.w2v_conv_k), 0.3, 0.0)]
+        specs += ln(p + "conv_module.depthwise_layer_norm.", H)
+        specs.append((p + "conv_module.pointwise_conv2.weight", (H, H, 1), lin, 0.0))
+        specs += ln(p + "final_layer_norm.", H)
+    return specs
+
+
+def weights_from_specs_cpu(specs, seed: int) -> dict[str, torch.Tensor]:
+    """fp32 CPU tensors of a spec list (the counter generator of this module)."""
+    out = {}
+    for name, shape, scale, off in specs:
+        v = synth_values(tensor_seed(seed, name), int(np.prod(shape)), scale)
+        t = torch.from_numpy(v).reshape(shape)
+        out[name] = t + off if off else t
+    return out
+
+
+def kaiser_sinc_filter(cutoff: float, half_width: float, kernel_size: int) -> torch.Tensor:
+    """The anti-aliasing filter of the encoder's Activation1d (filters.py:17-46, the julius /
+    alias-free-torch Kaiser-windowed sinc), computed with the same torch CPU ops in fp32."""
+    even = kernel_size % 2 == 0
+    half_size = kernel_size // 2
+    delta_f = 4 * half_width
+    A = 2.285 * (half_size - 1) * math.pi * delta_f + 7.95
+    if A > 50.0:
+        beta = 0.1102 * (A - 8.7)
+    elif A >= 21.0:
+        beta = 0.5842 * (A - 21) ** 0.4 + 0.07886 * (A - 21.0)
+    else:
+        beta = 0.0
+    window = torch.kaiser_window(kernel_size, beta=beta, periodic=False)
+    time = (torch.arange(-half_size, half_size) + 0.5) if even else (torch.arange(kernel_size) - half_size)
+    f = 2 * cutoff * window * torch.sinc(2 * cutoff * time)
+    return (f / f.sum()).float()
+
+
+def synthetic_wav(seed: int, n: int, sample_rate: int = 16000) -> np.ndarray:
+    """A deterministic speech-like test signal: three drifting partials + noise, peak ~0.5."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sample_rate
+    f0 = 120 + 40 * rng.random()
+    x = sum((0.3 / (h + 1)) * np.sin(2 * np.pi * f0 * (h + 1) * t * (1 + 0.05 * np.sin(2 * np.pi * 3 * t)) + rng.random())
+            for h in range(3))
+    x = x + 0.02 * rng.standard_normal(n)
+    return x.astype(np.float32)
+
+
 # ---------------------------------------------------------------------- codec weights ---
 
 def codec_tensor_specs(cfg: configs.CodecArch) -> list[tuple[str, tuple[int, ...], float, float]]:
