@@ -250,6 +250,15 @@ tts_status tts_encoder_encode(tts_engine* e, const float* wav, int64_t n_samples
                               int32_t n_frames, int32_t* codes, int32_t codes_cap, int32_t* n_codes,
                               float* pre_round);
 
+/* The same with w2v-bert-2.0 run here as well (its tensors given to tts_encoder_load under
+ * the reference Encoder's "wav2vec_model." prefix: transformers Wav2Vec2BertModel names,
+ * position_embeddings_type "relative_key", layers 0..15 used): features = the
+ * SeamlessM4TFeatureExtractor input_features of the padded waveform, host f32
+ * [n_frames][160] (the reference computes them on the CPU too, encoder.py:121-123). */
+tts_status tts_encoder_encode_features(tts_engine* e, const float* wav, int64_t n_samples, const float* features,
+                                       int32_t n_frames, int32_t* codes, int32_t codes_cap, int32_t* n_codes,
+                                       float* pre_round);
+
 #ifdef __cplusplus
 }
 #endif

@@ -271,6 +271,18 @@ tts_status tts_encoder_encode(tts_engine* e, const float* wav, int64_t n_samples
   });
 }
 
+tts_status tts_encoder_encode_features(tts_engine* e, const float* wav, int64_t n_samples, const float* features,
+                                       int32_t n_frames, int32_t* codes, int32_t codes_cap, int32_t* n_codes,
+                                       float* pre_round) {
+  return guarded([&] {
+    TTS_REQUIRE(e && wav && features && codes && n_codes, "null argument");
+    TTS_REQUIRE(n_samples >= 1 && n_samples < (1ll << 31) - 640, "bad waveform length");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    *n_codes = encoder_encode(E, wav, (int)n_samples, nullptr, n_frames, codes, codes_cap, pre_round, features);
+  });
+}
+
 tts_status tts_codec_samples_per_code(tts_engine* e, int32_t* out) {
   return guarded([&] {
     TTS_REQUIRE(e && out, "null argument");

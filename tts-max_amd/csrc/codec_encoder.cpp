@@ -12,6 +12,7 @@
 //   fusion Linear(2048) on [semantic | acoustic] -> project_in Linear(2048 -> 8) -> FSQ
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -33,6 +34,13 @@ struct EncConv {
 struct EncSnake { int C = 0; size_t a = 0, b = 0; };
 struct EncRU { EncSnake s1, s2; EncConv c1, c2; };
 struct EncBlock { EncRU ru[3]; EncSnake s; EncConv down; };
+// one w2v-bert conformer layer (offsets into the weight slab; every Linear [out][in])
+struct W2vLayer {
+  size_t ffn_ln[2][2], ffn_w1[2], ffn_b1[2], ffn_w2[2], ffn_b2[2];  // w2 / b2 pre-scaled by 0.5
+  size_t att_ln[2], qkv_w, qkv_b, out_w, out_b, dist;
+  size_t conv_ln[2], pw1, dw, dw_ln[2], pw2;
+  size_t fin_ln[2];
+};
 
 }  // namespace
 
@@ -45,6 +53,13 @@ struct AudioEncoder {
   DevBuf weights, planes, levels;
   std::map<const float*, const uint16_t*> bplanes;
   DevBuf x, y, z, win, sem, fused, proj, codes, pre;
+  // w2v-bert-2.0 up to hidden_states[16] (optional: loaded when its tensors are given)
+  bool w2v = false;
+  int wH = 1024, wFF = 4096, wFin = 160, wHeads = 16, wL = 64, wR = 8, wK = 31, wLayers = 16;
+  float wEps = 1e-5f;
+  size_t fp_ln[2] = {0, 0}, fp_w = 0, fp_b = 0;
+  std::vector<W2vLayer> wl;
+  DevBuf wx, wln, wbig, wqkv, watt, wfeat;
   const float* W(size_t off) const { return weights.as<float>() + off; }
 };
 
@@ -155,6 +170,64 @@ void encoder_load(Engine* e, const tts_tensor_desc* t, int n) {
   en->filt_up = put((const float*)tm.get(a + "conv_final_block.0.upsample.filter", {1, 1, 12}).data, 12);
   en->filt_dn = put((const float*)tm.get(a + "conv_final_block.0.downsample.lowpass.filter", {1, 1, 12}).data, 12);
 
+  // ---- w2v-bert (transformers Wav2Vec2BertModel state dict under "wav2vec_model.", as the
+  // reference Encoder holds it), when present
+  const std::string wp = "wav2vec_model.";
+  if (tm.m.count(wp + "feature_projection.projection.weight")) {
+    en->w2v = true;
+    const int H = en->wH, FF = en->wFF, Fi = en->wFin, hd = H / en->wHeads, K = en->wK;
+    auto vec = [&](const std::string& nm, std::initializer_list<int64_t> shp, float scale = 1.f) {
+      const tts_tensor_desc& d = tm.get(nm, shp);
+      std::vector<float> v((const float*)d.data, (const float*)d.data + numel(d));
+      if (scale != 1.f) for (auto& x : v) x *= scale;  // (x 0.5: exact)
+      return put(v.data(), v.size());
+    };
+    en->fp_ln[0] = vec(wp + "feature_projection.layer_norm.weight", {Fi});
+    en->fp_ln[1] = vec(wp + "feature_projection.layer_norm.bias", {Fi});
+    en->fp_w = vec(wp + "feature_projection.projection.weight", {H, Fi});
+    en->fp_b = vec(wp + "feature_projection.projection.bias", {H});
+    en->wl.resize(en->wLayers);
+    for (int l = 0; l < en->wLayers; ++l) {
+      W2vLayer& L = en->wl[l];
+      const std::string p = wp + "encoder.layers." + std::to_string(l) + ".";
+      for (int f = 0; f < 2; ++f) {
+        const std::string q = p + (f ? "ffn2" : "ffn1");
+        L.ffn_ln[f][0] = vec(q + "_layer_norm.weight", {H});
+        L.ffn_ln[f][1] = vec(q + "_layer_norm.bias", {H});
+        L.ffn_w1[f] = vec(q + ".intermediate_dense.weight", {FF, H});
+        L.ffn_b1[f] = vec(q + ".intermediate_dense.bias", {FF});
+        L.ffn_w2[f] = vec(q + ".output_dense.weight", {H, FF}, 0.5f);  // hidden * 0.5 + residual
+        L.ffn_b2[f] = vec(q + ".output_dense.bias", {H}, 0.5f);
+      }
+      L.att_ln[0] = vec(p + "self_attn_layer_norm.weight", {H});
+      L.att_ln[1] = vec(p + "self_attn_layer_norm.bias", {H});
+      {
+        std::vector<float> w((size_t)3 * H * H), b((size_t)3 * H);
+        const char* nm[3] = {"q", "k", "v"};
+        for (int i = 0; i < 3; ++i) {
+          const tts_tensor_desc& wd = tm.get(p + "self_attn.linear_" + nm[i] + ".weight", {H, H});
+          const tts_tensor_desc& bd = tm.get(p + "self_attn.linear_" + nm[i] + ".bias", {H});
+          memcpy(w.data() + (size_t)i * H * H, wd.data, (size_t)H * H * 4);
+          memcpy(b.data() + (size_t)i * H, bd.data, (size_t)H * 4);
+        }
+        L.qkv_w = put(w.data(), w.size());
+        L.qkv_b = put(b.data(), b.size());
+      }
+      L.out_w = vec(p + "self_attn.linear_out.weight", {H, H});
+      L.out_b = vec(p + "self_attn.linear_out.bias", {H});
+      L.dist = vec(p + "self_attn.distance_embedding.weight", {en->wL + en->wR + 1, hd});
+      L.conv_ln[0] = vec(p + "conv_module.layer_norm.weight", {H});
+      L.conv_ln[1] = vec(p + "conv_module.layer_norm.bias", {H});
+      L.pw1 = vec(p + "conv_module.pointwise_conv1.weight", {2 * H, H, 1});
+      L.dw = vec(p + "conv_module.depthwise_conv.weight", {H, 1, K});
+      L.dw_ln[0] = vec(p + "conv_module.depthwise_layer_norm.weight", {H});
+      L.dw_ln[1] = vec(p + "conv_module.depthwise_layer_norm.bias", {H});
+      L.pw2 = vec(p + "conv_module.pointwise_conv2.weight", {H, H, 1});
+      L.fin_ln[0] = vec(p + "final_layer_norm.weight", {H});
+      L.fin_ln[1] = vec(p + "final_layer_norm.bias", {H});
+    }
+  }
+
   en->weights.alloc(slab.size() * 4);
   HIP_CHECK(hipMemcpy(en->weights.p, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
   const int lv[8] = {4, 4, 4, 4, 4, 4, 4, 4};
@@ -172,6 +245,17 @@ void encoder_load(Engine* e, const tts_tensor_desc* t, int n) {
     }
     add(en->cf); add(en->sem_init); add(en->sem_c1); add(en->sem_c2); add(en->sem_final);
     bw.push_back({en->W(en->fus_w), (size_t)F * F});
+    for (auto& L : en->wl) {
+      const size_t H = en->wH, FF = en->wFF;
+      for (int f = 0; f < 2; ++f) {
+        bw.push_back({en->W(L.ffn_w1[f]), FF * H});
+        bw.push_back({en->W(L.ffn_w2[f]), FF * H});
+      }
+      bw.push_back({en->W(L.qkv_w), 3 * H * H});
+      bw.push_back({en->W(L.out_w), H * H});
+      bw.push_back({en->W(L.pw1), 2 * H * H});
+      bw.push_back({en->W(L.pw2), H * H});
+    }
     size_t tot = 0;
     for (auto& w : bw) tot += (3 * w.second + 127) & ~(size_t)127;
     en->planes.alloc(tot * 2);
@@ -197,12 +281,63 @@ void grow_buf(DevBuf& b, size_t bytes) {
 
 }  // namespace
 
-// codes[T] of one waveform (host fp32 [n] at 16 kHz) given its w2v-bert layer-16 features
-// (host fp32 [T][1024], T = the number of 320-sample hops of the padded waveform).
+// w2v-bert-2.0 hidden_states[16] of SeamlessM4T features (host [T][160]) into out (device
+// [T][1024]): feature projection (LayerNorm, Linear), then 16 conformer layers
+// (Wav2Vec2BertEncoderLayer: x + FFN1/2, x + attention, x + conv module, x + FFN2/2, final
+// LayerNorm), every contraction on the fp32-exact GEMM.
+static void w2v_forward(AudioEncoder& en, const float* feats, int T, float* out, hipStream_t s,
+                        const std::function<void(const float*, int, int, int, const float*, int, const float*, float*,
+                                                 int, const float*, int)>& gemm) {
+  const int H = en.wH, FF = en.wFF, Fi = en.wFin;
+  grow_buf(en.wfeat, (size_t)T * Fi * 4 * 2);
+  grow_buf(en.wln, (size_t)T * H * 4);
+  grow_buf(en.wbig, (size_t)T * FF * 4);
+  grow_buf(en.wqkv, (size_t)T * 3 * H * 4);
+  grow_buf(en.watt, (size_t)T * H * 4);
+  float* f = en.wfeat.as<float>();
+  float* fn = f + (size_t)T * Fi;
+  float* x = out;
+  float* ln = en.wln.as<float>();
+  float* big = en.wbig.as<float>();
+  float* qkv = en.wqkv.as<float>();
+  float* att = en.watt.as<float>();
+  HIP_CHECK(hipMemcpyAsync(f, feats, (size_t)T * Fi * 4, hipMemcpyHostToDevice, s));
+  launch_layernorm_f32(f, T, Fi, en.W(en.fp_ln[0]), en.W(en.fp_ln[1]), en.wEps, fn, s);
+  gemm(fn, T, Fi, Fi, en.W(en.fp_w), H, en.W(en.fp_b), x, H, nullptr, 0);
+  for (const W2vLayer& L : en.wl) {
+    for (int f2 = 0; f2 < 2; ++f2) {
+      if (f2 == 1) {  // 3. the convolution module (between the attention and FFN2)
+        launch_layernorm_f32(x, T, H, en.W(L.conv_ln[0]), en.W(L.conv_ln[1]), en.wEps, ln, s);
+        gemm(ln, T, H, H, en.W(L.pw1), 2 * H, nullptr, big, 2 * H, nullptr, 0);
+        launch_enc_glu(big, T, H, att, s);
+        launch_enc_dwconv(att, T, H, en.W(L.dw), en.wK, ln, s);
+        launch_layernorm_f32(ln, T, H, en.W(L.dw_ln[0]), en.W(L.dw_ln[1]), en.wEps, ln, s);
+        launch_enc_swish(ln, (long long)T * H, s);
+        gemm(ln, T, H, H, en.W(L.pw2), H, nullptr, x, H, x, 0);
+      }
+      // 1. / 4. x = x + FFN(LN(x)) / 2 (the 0.5 folded into output_dense at load)
+      launch_layernorm_f32(x, T, H, en.W(L.ffn_ln[f2][0]), en.W(L.ffn_ln[f2][1]), en.wEps, ln, s);
+      gemm(ln, T, H, H, en.W(L.ffn_w1[f2]), FF, en.W(L.ffn_b1[f2]), big, FF, nullptr, 1);
+      gemm(big, T, FF, FF, en.W(L.ffn_w2[f2]), H, en.W(L.ffn_b2[f2]), x, H, x, 0);
+      if (f2 == 0) {  // 2. x = x + attention(LN(x))
+        launch_layernorm_f32(x, T, H, en.W(L.att_ln[0]), en.W(L.att_ln[1]), en.wEps, ln, s);
+        gemm(ln, T, H, H, en.W(L.qkv_w), 3 * H, en.W(L.qkv_b), qkv, 3 * H, nullptr, 0);
+        launch_enc_relattn(qkv, T, en.wHeads, en.W(L.dist), en.wL, en.wR, att, s);
+        gemm(att, T, H, H, en.W(L.out_w), H, en.W(L.out_b), x, H, x, 0);
+      }
+    }
+    launch_layernorm_f32(x, T, H, en.W(L.fin_ln[0]), en.W(L.fin_ln[1]), en.wEps, x, s);
+  }
+}
+
+// codes[T] of one waveform (host fp32 [n] at 16 kHz) given either its w2v-bert layer-16
+// features (host fp32 [T][1024]) or its SeamlessM4T features (host fp32 [T][160], w2v-bert
+// run here), T = the number of 320-sample hops of the padded waveform.
 int encoder_encode(Engine* e, const float* wav, int n, const float* w2v, int T_w2v, int32_t* codes_out, int cap,
-                   float* pre_out) {
+                   float* pre_out, const float* feats) {
   TTS_REQUIRE(e->encoder != nullptr, "tts_encoder_load has not been called");
-  TTS_REQUIRE(wav && n >= 1 && w2v, "null argument");
+  TTS_REQUIRE(wav && n >= 1 && (w2v || feats), "null argument");
+  TTS_REQUIRE(!feats || e->encoder->w2v, "the encoder was loaded without its w2v-bert tensors");
   AudioEncoder& en = *e->encoder;
   hipStream_t s = e->stream;
   const int Np = n + (320 - n % 320);  // encode(): pad to a whole hop (+ a hop when whole)
@@ -221,15 +356,17 @@ int encoder_encode(Engine* e, const float* wav, int n, const float* w2v, int T_w
   grow_buf(en.codes, (size_t)T * 4);
   grow_buf(en.pre, (size_t)T * en.nl * 4);
 
-  auto gemm = [&](const float* A, int M, int K, int lda, const float* B, int N, const float* bias, float* C,
-                  int ldc, const float* resid) {
+  auto gemma = [&](const float* A, int M, int K, int lda, const float* B, int N, const float* bias, float* C,
+                   int ldc, const float* resid, int act) {
     GemmF32Args g;
     g.A = A; g.M = M; g.K = K; g.lda = lda; g.B = B; g.N = N; g.bias = bias;
     auto it = en.bplanes.find(B);
     if (it != en.bplanes.end()) g.Bp = it->second;
-    g.C = C; g.ldc = ldc; g.resid = resid;
+    g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
     launch_gemm_f32(g, s);
   };
+  auto gemm = [&](const float* A, int M, int K, int lda, const float* B, int N, const float* bias, float* C,
+                  int ldc, const float* resid) { gemma(A, M, K, lda, B, N, bias, C, ldc, resid, 0); };
   // Conv1d on x [Tin][cin] -> out [To][cout] (+ resid [To][cout]); returns To
   auto conv = [&](const EncConv& c, const float* x, int Tin, float* out, const float* resid) {
     const int To = (Tin + 2 * c.pad - c.dil * (c.k - 1) - 1) / c.stride + 1;
@@ -281,7 +418,8 @@ int encoder_encode(Engine* e, const float* wav, int n, const float* w2v, int T_w
   // ---- semantic path (features in, left half of the concatenation out)
   float* sx = en.sem.as<float>();
   float* sr = sx + (size_t)T * en.S;
-  HIP_CHECK(hipMemcpyAsync(sx, w2v, (size_t)T * en.S * 4, hipMemcpyHostToDevice, s));
+  if (feats) w2v_forward(en, feats, T, sx, s, gemma);
+  else HIP_CHECK(hipMemcpyAsync(sx, w2v, (size_t)T * en.S * 4, hipMemcpyHostToDevice, s));
   conv(en.sem_init, sx, T, sr, nullptr);
   launch_enc_relu(sr, (long long)T * en.S, s);  // ReLU(inplace=True): the skip sees it too
   conv(en.sem_c1, sr, T, sx, nullptr);

@@ -17,4 +17,12 @@ void launch_enc_relu(float* x, long long n, hipStream_t s);
 // ResidualFSQ (one quantizer) on z [T][nl] -> codes [T]; pre (optional) = the rounded values
 void launch_enc_fsq(const float* z, int T, int nl, const int* levels, int* codes, float* pre, hipStream_t s);
 
+// w2v-bert conformer ops: GLU over channel halves of [T][2C]; causal depthwise conv (left
+// pad k-1, w [C][k]); swish in place; relative-key self-attention (head dim 64, distance
+// embedding E [L + R + 1][64]) on fused qkv rows [3 * H * 64] -> [T][H * 64]
+void launch_enc_glu(const float* x, int T, int C, float* y, hipStream_t s);
+void launch_enc_dwconv(const float* x, int T, int C, const float* w, int k, float* y, hipStream_t s);
+void launch_enc_swish(float* x, long long n, hipStream_t s);
+void launch_enc_relattn(const float* qkv, int T, int H, const float* E, int L, int R, float* out, hipStream_t s);
+
 }  // namespace tts

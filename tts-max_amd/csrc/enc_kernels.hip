@@ -119,3 +119,164 @@ void launch_enc_fsq(const float* z, int T, int nl, const int* levels, int* codes
 }
 
 }  // namespace tts
+
+namespace tts {
+
+// ------------------------------------------------------------ w2v-bert conformer ops ----
+// (transformers models/wav2vec2_bert/modeling_wav2vec2_bert.py: Wav2Vec2BertConvolutionModule
+// 157-226, Wav2Vec2BertSelfAttention 229-330 with position_embeddings_type "relative_key")
+
+// GLU(dim=channels) on [T][2C]: a * sigmoid(b), a = the first C channels
+__global__ void enc_glu_kernel(const float* __restrict__ x, int T, int C, float* __restrict__ y) {
+  const long long total = (long long)T * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C), t = (int)(i / C);
+    const float a = x[(size_t)t * 2 * C + c], b = x[(size_t)t * 2 * C + C + c];
+    y[i] = a * (1.0f / (1.0f + expf(-b)));
+  }
+}
+
+void launch_enc_glu(const float* x, int T, int C, float* y, hipStream_t s) {
+  const long long g = ((long long)T * C + 255) / 256;
+  hipLaunchKernelGGL(enc_glu_kernel, dim3((unsigned)(g > 65536 ? 65536 : g)), dim3(256), 0, s, x, T, C, y);
+}
+
+// causal depthwise Conv1d(k, groups = C, no bias): the sequence padded by k-1 zeros on the
+// left only: y[t][c] = sum_j w[c][j] x[t - (k-1) + j][c]
+__global__ void enc_dwconv_kernel(const float* __restrict__ x, int T, int C, const float* __restrict__ w, int k,
+                                  float* __restrict__ y) {
+  const long long total = (long long)T * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C), t = (int)(i / C);
+    float acc = 0.f;
+    for (int j = 0; j < k; ++j) {
+      const int src = t - (k - 1) + j;
+      if (src >= 0) acc += w[(size_t)c * k + j] * x[(size_t)src * C + c];
+    }
+    y[i] = acc;
+  }
+}
+
+void launch_enc_dwconv(const float* x, int T, int C, const float* w, int k, float* y, hipStream_t s) {
+  const long long g = ((long long)T * C + 255) / 256;
+  hipLaunchKernelGGL(enc_dwconv_kernel, dim3((unsigned)(g > 65536 ? 65536 : g)), dim3(256), 0, s, x, T, C, w, k, y);
+}
+
+__global__ void enc_swish_kernel(float* __restrict__ x, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    x[i] = v * (1.0f / (1.0f + expf(-v)));
+  }
+}
+
+void launch_enc_swish(float* x, long long n, hipStream_t s) {
+  const long long g = (n + 255) / 256;
+  hipLaunchKernelGGL(enc_swish_kernel, dim3((unsigned)(g > 65536 ? 65536 : (g < 1 ? 1 : g))), dim3(256), 0, s, x, n);
+}
+
+// Self-attention with relative-key position scores, head dim 64, fp32:
+//   s[i][j] = q_i.k_j / 8 + q_i.E[clamp(j - i, -L, R) + L] / 8,  softmax over j,  o_i = sum p v
+// One workgroup = (head, 32 queries); thread (query tid / 8, part tid % 8) walks keys
+// part, part + 8, ... of each 64-key tile (K and V staged in LDS, rows padded to 68 floats:
+// conflict-free 16-B reads) with an online softmax, then the 8 parts of a query (adjacent
+// lanes) merge their (max, sum, o) in a fixed order.  qkv rows [3 * H * 64] (q | k | v, head
+// h at h * 64), out rows [H * 64].
+constexpr int RA_Q = 32, RA_KT = 64, RA_LD = 68, RA_NR = 73;
+__global__ __launch_bounds__(256) void enc_relattn_kernel(const float* __restrict__ qkv, int T, int H,
+                                                          const float* __restrict__ E, int L, int R,
+                                                          float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float Ks[RA_KT * RA_LD], Vs[RA_KT * RA_LD];
+  __shared__ float QE[RA_Q * RA_NR];
+  const int h = blockIdx.y, q0 = blockIdx.x * RA_Q;
+  const int tid = threadIdx.x, qi = tid >> 3, part = tid & 7;
+  const int qrow = min(q0 + qi, T - 1);
+  const int ld = 3 * H * 64;
+  const float* qp = qkv + (size_t)qrow * ld + h * 64;
+  float q[64];
+#pragma unroll
+  for (int d = 0; d < 64; d += 4) {
+    const float4 v = *(const float4*)(qp + d);
+    q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
+  }
+  // q . E_r for the 73 distance rows: thread (qi, part) takes r = part, part + 8, ...
+  for (int r = part; r < L + R + 1; r += 8) {
+    const float* e = E + (size_t)r * 64;
+    float acc = 0.f;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) acc += q[d] * e[d];
+    QE[qi * RA_NR + r] = acc;
+  }
+  float m = -INFINITY, l = 0.f, o[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) o[d] = 0.f;
+  const int i = q0 + qi;
+  for (int k0 = 0; k0 < T; k0 += RA_KT) {
+    __syncthreads();
+    for (int e = tid; e < RA_KT * 16; e += 256) {  // 64 keys x 16 float4 each of K and V
+      const int kr = e >> 4, c4 = (e & 15) * 4;
+      const int src = min(k0 + kr, T - 1);
+      *(float4*)(Ks + kr * RA_LD + c4) = *(const float4*)(qkv + (size_t)src * ld + H * 64 + h * 64 + c4);
+      *(float4*)(Vs + kr * RA_LD + c4) = *(const float4*)(qkv + (size_t)src * ld + 2 * H * 64 + h * 64 + c4);
+    }
+    __syncthreads();
+    for (int kk = part; kk < RA_KT; kk += 8) {
+      const int j = k0 + kk;
+      if (j >= T) break;
+      const float* kr = Ks + kk * RA_LD;
+      float dot = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; d += 4) {
+        const float4 kv = *(const float4*)(kr + d);
+        dot += q[d] * kv.x + q[d + 1] * kv.y + q[d + 2] * kv.z + q[d + 3] * kv.w;
+      }
+      int dist = j - i;
+      dist = dist < -L ? -L : (dist > R ? R : dist);
+      const float s = dot / 8.0f + QE[qi * RA_NR + dist + L] / 8.0f;
+      if (s > m) {
+        const float sc = expf(m - s);
+        l *= sc;
+#pragma unroll
+        for (int d = 0; d < 64; ++d) o[d] *= sc;
+        m = s;
+      }
+      const float p = expf(s - m);
+      l += p;
+      const float* vr = Vs + kk * RA_LD;
+#pragma unroll
+      for (int d = 0; d < 64; d += 4) {
+        const float4 vv = *(const float4*)(vr + d);
+        o[d] += p * vv.x; o[d + 1] += p * vv.y; o[d + 2] += p * vv.z; o[d + 3] += p * vv.w;
+      }
+    }
+  }
+  // merge the 8 parts of the query (lanes 8qi .. 8qi+7 of the wave), partner order fixed
+#pragma unroll
+  for (int off = 1; off < 8; off <<= 1) {
+    const float m2 = __shfl_xor(m, off, 64), l2 = __shfl_xor(l, off, 64);
+    const float mn = fmaxf(m, m2);
+    const float a = (m == -INFINITY) ? 0.f : expf(m - mn), b = (m2 == -INFINITY) ? 0.f : expf(m2 - mn);
+    l = l * a + l2 * b;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) {
+      const float o2 = __shfl_xor(o[d], off, 64);
+      o[d] = o[d] * a + o2 * b;
+    }
+    m = mn;
+  }
+  if (q0 + qi < T) {
+    float* op = out + (size_t)(q0 + qi) * H * 64 + h * 64 + part * 8;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      float v = 0.f;
+#pragma unroll
+      for (int e = 0; e < 64; ++e) v = (e == part * 8 + d) ? o[e] : v;  // (register-indexed select)
+      op[d] = v / l;
+    }
+  }
+}
+
+void launch_enc_relattn(const float* qkv, int T, int H, const float* E, int L, int R, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(enc_relattn_kernel, dim3((T + RA_Q - 1) / RA_Q, H), dim3(256), 0, s, qkv, T, H, E, L, R, out);
+}
+
+}  // namespace tts

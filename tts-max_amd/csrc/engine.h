@@ -174,7 +174,7 @@ int codec_samples_per_code(Engine* e);
 // the prompt-audio encoder (codec_encoder.cpp)
 void encoder_load(Engine* e, const tts_tensor_desc* t, int n);
 int encoder_encode(Engine* e, const float* wav, int n, const float* w2v, int T_w2v, int32_t* codes, int cap,
-                   float* pre);
+                   float* pre, const float* feats = nullptr);
 void encoder_destroy(AudioEncoder* a);
 void codec_destroy(Codec* c);
 

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "tts_codec_samples_per_code",
     "tts_encoder_load",
     "tts_encoder_encode",
+    "tts_encoder_encode_features",
     "tts_synth_fill",
     "tts_op_retile",
     "tts_op_wgemm",
@@ -176,6 +177,8 @@ def load_library() -> ctypes.CDLL:
         "tts_encoder_load": (I32, [P, P, I32]),
         "tts_encoder_encode": (I32, [P, ctypes.POINTER(F32), ctypes.c_int64, ctypes.POINTER(F32), I32, pi32, I32,
                                      pi32, ctypes.POINTER(F32)]),
+        "tts_encoder_encode_features": (I32, [P, ctypes.POINTER(F32), ctypes.c_int64, ctypes.POINTER(F32), I32,
+                                              pi32, I32, pi32, ctypes.POINTER(F32)]),
         "tts_synth_fill": (I32, [P, I32, I64, U64, F32, P]),
         "tts_op_retile": (I32, [P, P, I32, I32, I32, P]),
         "tts_op_wgemm": (I32, [P, I32, I32, I32, P, I32, P, F32, P, I32, P, I32, P]),

@@ -6,13 +6,13 @@ Drop-in for tts/core/codec/encoding.py: ``AudioEncoderInterface`` (9-26), ``Audi
 
 Split of the work (the reference runs it all in ``Encoder.encode``, encoder.py:115-128):
 
-* host (CPU, as the reference): the padding and transformers' SeamlessM4TFeatureExtractor;
-* w2v-bert-2.0 up to hidden_states[16] (the reference's ``wav2vec_model``): transformers'
-  Wav2Vec2BertModel on the same GPU through PyTorch — the one part of the encoder not yet a
-  HIP kernel (DESIGN §8);
-* everything after it — AcousticEncoder over the waveform (Snake with the anti-aliased
-  2x filters, dilated and strided convolutions), SemanticEncoder, fusion, ResidualFSQ
-  quantisation — in fp32 HIP kernels through ``tts_encoder_encode``.
+* host (CPU, as the reference): the padding and transformers' SeamlessM4TFeatureExtractor
+  (the reference's own feature extractor class);
+* everything after it in fp32 HIP kernels through ``tts_encoder_encode_features``:
+  w2v-bert-2.0 up to hidden_states[16] (feature projection, 16 conformer layers with
+  relative-key attention and the causal depthwise-conv module), AcousticEncoder over the
+  waveform (Snake with the anti-aliased 2x filters, dilated and strided convolutions),
+  SemanticEncoder, fusion, ResidualFSQ quantisation.
 """
 
 from __future__ import annotations
@@ -54,8 +54,10 @@ def pad_like_reference(wav: torch.Tensor, hop: int = 320) -> tuple[torch.Tensor,
 class MI355XAudioEncoder(AudioEncoderInterface):
     """One encoder resident on one MI355X (its own engine)."""
 
-    def __init__(self, weights: dict[str, torch.Tensor], w2v_model: torch.nn.Module, feature_extractor,
+    def __init__(self, weights: dict[str, torch.Tensor], feature_extractor,
                  arch: configs.EncoderArch = configs.ENCODER, device: int = 0):
+        """weights: the reference Encoder's state dict (its own modules and, under
+        "wav2vec_model.", the w2v-bert-2.0 tensors) plus the anti-aliasing filter buffers."""
         self.arch = arch
         self.device = torch.device("cuda", device)
         self._lib = _lib.load_library()
@@ -66,7 +68,6 @@ class MI355XAudioEncoder(AudioEncoderInterface):
         descs, keep = _lib.make_descs(tensors)
         _lib.check(self._lib.tts_encoder_load(self._h, descs, len(tensors)))
         del keep
-        self._w2v = w2v_model.to(self.device).eval()
         self._fe = feature_extractor
 
     @classmethod
@@ -80,13 +81,10 @@ class MI355XAudioEncoder(AudioEncoderInterface):
         f = synth.kaiser_sinc_filter(0.25, 0.3, 12).view(1, 1, 12)
         w["acoustic_encoder.conv_final_block.0.upsample.filter"] = f
         w["acoustic_encoder.conv_final_block.0.downsample.lowpass.filter"] = f.clone()
-        cfg = transformers.Wav2Vec2BertConfig(**arch.w2v_hf_config())
-        with torch.device("meta"):
-            w2v = transformers.Wav2Vec2BertModel(cfg)
-        w2v = w2v.to_empty(device="cpu")
-        w2v.load_state_dict(synth.weights_from_specs_cpu(synth.w2v_tensor_specs(arch), seed + 1), strict=True)
+        for k, v in synth.weights_from_specs_cpu(synth.w2v_tensor_specs(arch), seed + 1).items():
+            w["wav2vec_model." + k] = v
         fe = transformers.SeamlessM4TFeatureExtractor(padding_value=1.0)
-        return cls(w, w2v, fe, arch=arch, device=device)
+        return cls(w, fe, arch=arch, device=device)
 
     @property
     def sample_rate(self) -> int:
@@ -96,13 +94,12 @@ class MI355XAudioEncoder(AudioEncoderInterface):
     def token_rate(self) -> int:
         return self.arch.token_rate
 
-    @torch.no_grad()
-    def w2v_features(self, wav: torch.Tensor) -> np.ndarray:
-        """w2v-bert-2.0 hidden_states[16] of the reference-padded waveform [1, N] -> [T, 1024]."""
+    def features(self, wav: torch.Tensor) -> np.ndarray:
+        """SeamlessM4TFeatureExtractor input_features of the reference-padded waveform [1, N]
+        -> [T, 160] (host, as encoder.py:121-123)."""
         _, audio_pad = pad_like_reference(wav.reshape(1, -1), self.arch.hop)
         feat = self._fe(audio_pad, sampling_rate=self.arch.sample_rate, return_tensors="pt").data["input_features"]
-        out = self._w2v(feat.to(self.device), output_hidden_states=True).hidden_states[16]
-        return np.ascontiguousarray(out[0].float().cpu().numpy())
+        return np.ascontiguousarray(feat[0].float().numpy())
 
     def encode_with_features(self, wav: np.ndarray, w2v: np.ndarray, return_pre: bool = False):
         """The HIP part of Encoder.encode: waveform [N] + its w2v-bert features [T, 1024] ->
@@ -120,12 +117,28 @@ class MI355XAudioEncoder(AudioEncoderInterface):
             pre.ctypes.data_as(f32p) if return_pre else None))
         return (codes[: n.value], pre) if return_pre else codes[: n.value]
 
+    def encode_from_features(self, wav: np.ndarray, feats: np.ndarray, return_pre: bool = False):
+        """Waveform [N] + its SeamlessM4T features [T, 160] -> codes [T]: w2v-bert and the
+        rest of the encoder in HIP (tts_encoder_encode_features)."""
+        wav = np.ascontiguousarray(wav, dtype=np.float32).reshape(-1)
+        feats = np.ascontiguousarray(feats, dtype=np.float32)
+        T = feats.shape[0]
+        codes = np.zeros(T, dtype=np.int32)
+        pre = np.zeros((T, len(self.arch.levels)), dtype=np.float32) if return_pre else None
+        n = ctypes.c_int32()
+        f32p = ctypes.POINTER(ctypes.c_float)
+        _lib.check(self._lib.tts_encoder_encode_features(
+            self._h, wav.ctypes.data_as(f32p), wav.size, feats.ctypes.data_as(f32p), T,
+            codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), T, ctypes.byref(n),
+            pre.ctypes.data_as(f32p) if return_pre else None))
+        return (codes[: n.value], pre) if return_pre else codes[: n.value]
+
     @torch.no_grad()
     def encode(self, wav: torch.Tensor) -> torch.Tensor:
         """AudioEncoder.encode (encoding.py:42-45 -> encoder.py:115-128): wav [1, N] at
         16 kHz -> codes [T] (int64, CPU; the reference's .squeeze() of the [1, 1, T] codes)."""
         wav = wav.reshape(1, -1)
-        codes = self.encode_with_features(wav[0].float().cpu().numpy(), self.w2v_features(wav))
+        codes = self.encode_from_features(wav[0].float().cpu().numpy(), self.features(wav))
         return torch.from_numpy(codes.astype(np.int64))
 
     def close(self):
