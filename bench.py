@@ -291,6 +291,26 @@ def main():
         sec["stream_bs8"] = dict(p50_first_audio_ms=round(1000 * float(np.median(firsts)), 3),
                                  chunk_codes=25, left_context_codes=25,
                                  codes_per_s=round(8 * N / float(np.median(totals)), 2))
+        # the prompt-audio encoder on the prompt's length of audio: host
+        # SeamlessM4T features, then w2v-bert + acoustic + semantic + FSQ in HIP
+        from tts_amd.encoder import MI355XAudioEncoder
+
+        enc = MI355XAudioEncoder.synthetic(device=dev.index or 0)
+        wav_p = torch.from_numpy(synth.synthetic_wav(5, args.prompt_codes * 320))[None]
+        t = time.perf_counter()
+        feats = enc.features(wav_p)
+        feat_ms = (time.perf_counter() - t) * 1000
+        enc.encode_from_features(wav_p[0].numpy(), feats)
+        t = time.perf_counter()
+        for _ in range(3):
+            enc_codes = enc.encode_from_features(wav_p[0].numpy(), feats)
+        sec["encoder"] = dict(prompt_s=round(wav_p.shape[1] / 16000, 3), frames=int(enc_codes.size),
+                              encode_ms=round((time.perf_counter() - t) / 3 * 1000, 3),
+                              host_feature_ms=round(feat_ms, 3),
+                              note="w2v-bert-2.0 (16 layers) + acoustic + semantic + fusion + FSQ in HIP (fp32); "
+                                   "SeamlessM4T features on the host CPU as the reference computes them")
+        enc.close()
+        del enc
         log(f"secondary: {sec}")
 
     cpu = None

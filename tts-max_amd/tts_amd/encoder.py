@@ -65,6 +65,9 @@ class MI355XAudioEncoder(AudioEncoderInterface):
         _lib.check(self._lib.tts_engine_create(device, ctypes.byref(h)))
         self._h = h
         tensors = {k: v.detach().float().cpu().contiguous() for k, v in weights.items()}
+        f = synth.kaiser_sinc_filter(0.25, 0.3, 12).view(1, 1, 12)  # the filters' buffers (filters.py)
+        tensors.setdefault("acoustic_encoder.conv_final_block.0.upsample.filter", f)
+        tensors.setdefault("acoustic_encoder.conv_final_block.0.downsample.lowpass.filter", f.clone())
         descs, keep = _lib.make_descs(tensors)
         _lib.check(self._lib.tts_encoder_load(self._h, descs, len(tensors)))
         del keep
@@ -77,11 +80,9 @@ class MI355XAudioEncoder(AudioEncoderInterface):
         tests/golden/encoder_16k.npz was made with."""
         import transformers
 
-        w = synth.weights_from_specs_cpu(synth.encoder_tensor_specs(arch), seed)
-        f = synth.kaiser_sinc_filter(0.25, 0.3, 12).view(1, 1, 12)
-        w["acoustic_encoder.conv_final_block.0.upsample.filter"] = f
-        w["acoustic_encoder.conv_final_block.0.downsample.lowpass.filter"] = f.clone()
-        for k, v in synth.weights_from_specs_cpu(synth.w2v_tensor_specs(arch), seed + 1).items():
+        dev = torch.device("cuda", device)
+        w = synth.weights_from_specs_device(synth.encoder_tensor_specs(arch), seed, dev)
+        for k, v in synth.weights_from_specs_device(synth.w2v_tensor_specs(arch), seed + 1, dev).items():
             w["wav2vec_model." + k] = v
         fe = transformers.SeamlessM4TFeatureExtractor(padding_value=1.0)
         return cls(w, fe, arch=arch, device=device)
@@ -167,3 +168,46 @@ class CachingAudioEncoder:
         codes = self._encoder.encode(prompt_wav).cpu().tolist()
         self._prompt_encoding_cache[prompt_id] = codes
         return codes
+
+
+# xcodec2 checkpoint prefixes -> the reference Encoder's module names (encoder.py:87-105)
+_XCODEC2_PREFIXES = (("CodecEnc.", "acoustic_encoder."), ("generator.quantizer.", "quantizer."),
+                     ("SemanticEncoder_module.", "semantic_encoder."), ("fc_prior.", "fusion_layer."))
+
+
+def load_encoder_checkpoint(path: str) -> dict[str, torch.Tensor]:
+    """Encoder.load_from_checkpoint (encoder.py:80-113) with weights_only=True (no pickled
+    code runs): an xcodec2 {"state_dict": ...} checkpoint has its four prefixes mapped onto the
+    Encoder's modules (other keys ignored, as there); anything else is the Encoder's own state
+    dict (which may include "wav2vec_model.*")."""
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    if "state_dict" in ckpt:
+        out = {}
+        for k, v in ckpt["state_dict"].items():
+            for src, dst in _XCODEC2_PREFIXES:
+                if k.startswith(src):
+                    out[dst + k[len(src):]] = v
+        return out
+    return dict(ckpt)
+
+
+def create(model_path: str, device: "torch.device | str | int | None" = 0,
+           w2v_path: str | None = None) -> MI355XAudioEncoder:
+    """encoding.create (75-80): the encoder from its checkpoint.  The reference loads
+    facebook/w2v-bert-2.0 and its feature extractor from the hub (encoder.py:50-56); offline
+    they come from a local copy of that model directory (`w2v_path`: config.json,
+    safetensors weights, preprocessor_config.json) unless the checkpoint already holds
+    "wav2vec_model.*"."""
+    import transformers
+
+    w = load_encoder_checkpoint(model_path)
+    if not any(k.startswith("wav2vec_model.") for k in w):
+        if w2v_path is None:
+            raise ValueError("the checkpoint has no w2v-bert weights: pass w2v_path (a local facebook/w2v-bert-2.0)")
+        m = transformers.Wav2Vec2BertModel.from_pretrained(w2v_path)
+        for k, v in m.state_dict().items():
+            w["wav2vec_model." + k] = v
+    fe = (transformers.SeamlessM4TFeatureExtractor.from_pretrained(w2v_path) if w2v_path
+          else transformers.SeamlessM4TFeatureExtractor(padding_value=1.0))
+    dev = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+    return MI355XAudioEncoder(w, fe, device=dev.index or 0)

@@ -326,6 +326,22 @@ def weights_from_specs_cpu(specs, seed: int) -> dict[str, torch.Tensor]:
     return out
 
 
+def weights_from_specs_device(specs, seed: int, device) -> dict[str, torch.Tensor]:
+    """The same fp32 values generated on the GPU (tts_synth_fill) and returned on the host
+    (bit-identical to weights_from_specs_cpu, a few seconds instead of minutes for w2v-bert)."""
+    from . import _lib
+
+    lib = _lib.load_library()
+    out = {}
+    for name, shape, scale, off in specs:
+        t = torch.empty(shape, dtype=torch.float32, device=device)
+        _lib.check(lib.tts_synth_fill(t.data_ptr(), _lib.DT_F32, int(np.prod(shape)), tensor_seed(seed, name), scale,
+                                      _lib.stream_ptr()))
+        out[name] = t + off if off else t
+    torch.cuda.synchronize()
+    return {k: v.cpu() for k, v in out.items()}
+
+
 def kaiser_sinc_filter(cutoff: float, half_width: float, kernel_size: int) -> torch.Tensor:
     """The anti-aliasing filter of the encoder's Activation1d (filters.py:17-46, the julius /
     alias-free-torch Kaiser-windowed sinc), computed with the same torch CPU ops in fp32."""
