@@ -160,6 +160,17 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
     static const bool one_round = !(getenv("TTS_SLICED_GRID") && !atoi(getenv("TTS_SLICED_GRID")));
     if (one_round) p.grid = std::max(1, std::min(p.grid, (num_cu + p.sp.kc - 1) / p.sp.kc));
   }
+  // A matrix with at most half a unit per CU (TTS-1 o_proj and down at 1..16 rows: 128 units)
+  // streams each unit as two 8-column halves on twice the workgroups: every CU pulls half
+  // the bytes.  TTS_CSPLIT=0: off; =2: also at 17..64 rows.
+  static const int csplit_mode = getenv("TTS_CSPLIT") ? atoi(getenv("TTS_CSPLIT")) : 1;
+  const int units = (N / 16) / ng;
+  const int upw = w / ks;
+  if (csplit_mode > 0 && (M <= 16 || csplit_mode == 2) && !p.sliced && p.a_lds &&
+      (epi == EPI_STORE || epi == EPI_RESID) && p.grid * upw >= units && 2 * units <= num_cu * upw) {
+    p.csplit = 2;
+    p.grid = (2 * units + upw - 1) / upw;
+  }
   return p;
 }
 
@@ -178,11 +189,19 @@ bool wgemm_supported(int M, int N, int K, int epi) {
   return M >= 1 && M <= 64 && (N % (16 * NG)) == 0 && (K % 256) == 0;
 }
 
-void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p, int epi, bool norm, hipStream_t s) {
+void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p_in, int epi, bool norm, hipStream_t s) {
   WgemmArgs a = a_in;
+  WgemmPlan p = p_in;
+  if (p.csplit == 2 && a.fattn_wgs) {  // the fused QKV + attention launch keeps whole units
+    p.csplit = 1;
+    p.grid = p.sp.grid;
+  }
   a.ur = p.sp.ur();
   a.kc = p.sp.kc;
   a.sliced = p.sliced ? 1 : 0;
+  a.csplit = p.csplit;
+  if (a.csplit == 2 && epi != EPI_STORE && epi != EPI_RESID)
+    throw std::runtime_error("wgemm: column split only for plain store / residual launches");
   static const int diag = getenv("TTS_WGEMM_DIAG") ? atoi(getenv("TTS_WGEMM_DIAG")) : 0;
   a.diag = diag;
   if (p.sliced) {

@@ -144,7 +144,13 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   const int ugrp = wave / KSPLIT;
   const int M = a.M;
   const int mtn = (M + 15) >> 4;
-  const int units = (a.N >> 4) / NG;
+  // column split (a.csplit = 2, store / residual epilogues): work unit u is half u & 1 of
+  // layout unit u >> 1; its waves load only that half's 8 columns of every tile (the other
+  // lanes re-read the same 128-B pieces, no extra HBM bytes), so a matrix of 128 units
+  // streams on 256 workgroups
+  const int cs2 = a.csplit == 2 ? 1 : 0;
+  const int bunits = (a.N >> 4) / NG;  // layout units
+  const int units = bunits << cs2;     // work units
   // K layout (StreamPlan::kc chunks, chunk-major): a wave's K part is kt_pc k-tiles of every
   // chunk; its stage st covers k-tiles kt(st) .. +KU-1 of chunk st / Sc.  K-sliced launches
   // (a.sliced) run chunk blockIdx.y only: a.K = one chunk, A = that chunk's columns.
@@ -166,9 +172,9 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // stage st of the wave's item of unit uu = NG*KU consecutive tiles from this tile index
   const int ur = a.ur;
   auto stile = [&](int uu, int st) -> long long {
-    uu = min(uu, units - 1);
+    uu = min(uu, units - 1) >> cs2;
     const int r = uu / ur, ui = uu - r * ur;
-    const int nr = min(ur, units - r * ur);
+    const int nr = min(ur, bunits - r * ur);
     return (long long)r * ur * KT * NG + (((long long)(st + st_off) * nr + ui) * KSPLIT + kpart) * NG * KU;
   };
   const int S = a.sliced ? Sc : kc * Sc;  // stages per item in this launch
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {  // (no mt < mtn test: loads behind a branch cost exact vmcnt)
       const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
-      if constexpr (EPI == EPI_RESID) rre[mt][r] = a.resid[(size_t)m * a.ldo + u_first * 16 + (lane & 15)];
+      if constexpr (EPI == EPI_RESID) rre[mt][r] = a.resid[(size_t)m * a.ldo + (u_first >> cs2) * 16 + (lane & 15)];
       if constexpr (EPI == EPI_LOGITS) {
         eosr[mt][r] = a.eos_mask[m];
         seen_cur[mt][r] = a.seen[(size_t)m * a.seen_stride + (u_first >> 1)];
@@ -242,7 +248,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 
   // ---- then the weight stream
   // stage st of the wave's item of unit uu: NG*KU consecutive tiles (StreamPlan layout)
-  auto sptr = [&](int uu, int st) { return (const u32x4_t*)a.w + stile(uu, st) * 64 + lane; };
+  auto sptr = [&](int uu, int st) {
+    const int ls = cs2 ? ((lane & ~8) | ((min(uu, units - 1) & 1) << 3)) : lane;
+    return (const u32x4_t*)a.w + stile(uu, st) * 64 + ls;
+  };
   // Register ring of R stages (S = stages per item, S % R == 0): the first R stages of the
   // wave's stream are in flight before the prologue runs; consuming a slot refills it with
   // the stage R positions later (next unit's stages once this unit's are all issued).
@@ -525,8 +534,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
 
     // ---- epilogue (lane owns column n, rows m = mt*16 + 4*(lane>>4) + r)
-    if (kpart == 0 && active) {
-      const int n = u * 16 + (lane & 15);
+    if (kpart == 0 && active && (!cs2 || ((lane >> 3) & 1) == (u & 1))) {
+      const int n = (u >> cs2) * 16 + (lane & 15);
 #pragma unroll
       for (int mt = 0; mt < MT_MAX; ++mt) {
         if (mt >= mtn) continue;

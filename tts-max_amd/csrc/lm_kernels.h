@@ -98,6 +98,7 @@ struct WgemmArgs {
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
   int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
+  int csplit = 1;     // 2: each 16-column unit runs as two 8-column halves (twice the workgroups; filled in by launch_wgemm)
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
 };
 
@@ -107,6 +108,7 @@ struct WgemmPlan {
   int grid = 1;
   bool a_lds = true;
   bool sliced = false;  // one K chunk per workgroup (grid.y = sp.kc) + combine kernel
+  int csplit = 1;       // 2: units split into 8-column halves over twice the workgroups
 };
 
 // Row-major W [N][K] -> tiles of the matrix's stream plan.  The destination matrix has
