@@ -1,0 +1,55 @@
+"""In-kernel timeline of the one-row decode kernels (run on the MI355X box): loads the
+diagnostic library (make -C tts-max_amd/csrc stamps: -DTTS_STAMPS), runs one launch of each
+kernel through bench_kernel and prints, per kernel, the workgroups' clock stamps (100 MHz,
+us relative to the earliest entry): entry / after prologue / first unit streamed / first
+unit's epilogue done (GEMM workgroups), entry / granules seen / before attention / after
+attention (fused attention workgroups).  usage: python scripts/stamp_probe.py [CTX]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tts-max_amd"))
+from tts_amd import _lib, configs  # noqa: E402
+
+_lib.LIB_PATH = os.path.join(ROOT, "tts-max_amd", "tts_amd", "libtts_mi355x_stamps.so")
+lib = _lib.load_library()
+from tts_amd.speechlm import MI355XSpeechLM  # noqa: E402
+
+ctx = int(sys.argv[1]) if len(sys.argv) > 1 else 450
+m = MI355XSpeechLM.synthetic(configs.TTS1, max_batch=1, max_seq_len=1040)
+N = 1 << 16
+buf = np.zeros(N, dtype=np.uint64)
+f = lib.tts_debug_stamps
+f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+
+
+def q(v):
+    return "/".join(f"{x:5.2f}" for x in (np.min(v), np.median(v), np.max(v)))
+
+
+for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn"):
+    for rep in range(3):
+        m.bench_kernel(k, rows=1, ctx=ctx, iters=1)
+        assert f(buf.ctypes.data, N) == 0
+    t = buf.astype(np.int64)
+    if k == "attention":
+        st = t[4096:4096 + 8 * 8].reshape(-1, 8)
+    else:
+        st = t[:4096].reshape(-1, 8)
+    st = st[st[:, 0] > 0]
+    t0 = st[:, 0].min()
+    us = (st - t0) / 100.0
+    us[st == 0] = np.nan
+    print(f"{k} ctx={ctx}: {len(st)} workgroups (min/median/max us from first entry)")
+    if k == "qkv_attn":
+        proj, cons = us[:-8], us[-8:]  # (the attention workgroups are the grid's last 8)
+        print(f"  projection  entry {q(proj[:, 0])}  prologue {q(proj[:, 1])}  streamed {q(proj[:, 2])}  epilogue {q(proj[:, 3])}")
+        print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  attended {q(cons[:, 3])}")
+    elif k == "attention":
+        print(f"  entry {q(us[:, 0])}  rope {q(us[:, 2])}  attended {q(us[:, 3])}")
+    else:
+        print(f"  entry {q(us[:, 0])}  prologue {q(us[:, 1])}  streamed {q(us[:, 2])}  epilogue {q(us[:, 3])}")
+    sys.stdout.flush()

@@ -10,8 +10,24 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
 #define TTS_DEV __device__ __forceinline__
+// Diagnostic build only (make stamps: -DTTS_STAMPS, scripts/stamp_probe.py): thread 0 of a
+// workgroup writes the chip-wide 100 MHz clock to stamps[slot].  Compiled out otherwise.
+#ifdef TTS_STAMPS
+#define TTS_STAMP(buf, slot) \
+  do { if ((buf) && threadIdx.x == 0) (buf)[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TTS_STAMP(buf, slot) do {} while (0)
+#endif
 
 // bf16 -> fp32 is exact: the bf16 bits are the top half of the fp32 pattern.
+// Workgroup barrier ordering LDS only: unlike __syncthreads (which waits for every
+// outstanding global load first, vmcnt(0)), the weight stream a wave has in flight stays in
+// flight across it.  For hand-offs through LDS only.
+TTS_DEV void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 TTS_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 TTS_DEV float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 TTS_DEV float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }

@@ -68,6 +68,8 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
   const size_t kvbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
   const bf16_t* kc = a.kcache + kvbase;
   const bf16_t* vtc = a.vtcache + kvbase;
+  unsigned long long* stp = a.stamps ? a.stamps + 4096 + (size_t)blockIdx.x * 8 : nullptr;
+  TTS_STAMP(stp, 0);
   // this wave's first-pass fragments before anything else (vmcnt retires in issue order)
   u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
   if (wave * PW < ctx) {
@@ -88,9 +90,11 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
       vnew[d] = qrow[a.H * D + a.KVH * D + kvh * D + d];
     }
   }
-  __syncthreads();
+  lds_barrier();
+  TTS_STAMP(stp, 2);
   dec_attend<D, PW, NW>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
                         a.out + (size_t)row * a.H * D + kvh * DEC_G * D);
+  TTS_STAMP(stp, 3);
   // the new position into the cache, after this workgroup's reads (no other workgroup reads
   // this (slot, kv head))
   if (tid < D) {

@@ -80,20 +80,25 @@ TTS_DEV void dec_load_v(const bf16_t* vtc, int S, int base, int lane,
 
 // The new position (ctx - 1) is not in the cache yet: its roped k / its v (LDS, bf16) replace
 // the stale row / column elements in the fragments; V elements past ctx are zeroed (their p is
-// 0, and 0 * NaN from never-written memory would poison the sum).
+// 0, and 0 * NaN from never-written memory would poison the sum).  Branch-free: the LDS values
+// are read unconditionally and merged with bit masks (a select whose operand is a load is
+// otherwise turned into a branch around the load, and every such branch also drains vmcnt).
+TTS_DEV uint32_t bits_sel(uint32_t mask, uint32_t a, uint32_t b) { return (a & mask) | (b & ~mask); }
 template <int D, int PW>
 TTS_DEV void dec_patch_k(int base, int ctx, int lane, const bf16_t* knew,
                          u32x4_t (&kf)[DecShape<D, PW>::MT][DecShape<D, PW>::KS]) {
   using C = DecShape<D, PW>;
   const int c = lane & 15, g = lane >> 4, pn = ctx - 1;
+  u32x4_t kn[C::KS];
+#pragma unroll
+  for (int ks = 0; ks < C::KS; ++ks) kn[ks] = *(const u32x4_t*)(knew + 32 * ks + 8 * g);
 #pragma unroll
   for (int mt = 0; mt < C::MT; ++mt) {
-    const bool mine = dec_pos(base, mt, c) == pn;
+    const uint32_t m = dec_pos(base, mt, c) == pn ? 0xffffffffu : 0u;
 #pragma unroll
-    for (int ks = 0; ks < C::KS; ++ks) {
-      const u32x4_t kn = *(const u32x4_t*)(knew + 32 * ks + 8 * g);
-      kf[mt][ks] = mine ? kn : kf[mt][ks];
-    }
+    for (int ks = 0; ks < C::KS; ++ks)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) kf[mt][ks][q] = bits_sel(m, kn[ks][q], kf[mt][ks][q]);
   }
 }
 template <int D, int PW>
@@ -101,22 +106,25 @@ TTS_DEV void dec_patch_v(int base, int ctx, int lane, const bf16_t* vnew,
                          u32x4_t (&vf)[DecShape<D, PW>::PS][DecShape<D, PW>::DT]) {
   using C = DecShape<D, PW>;
   const int c = lane & 15, g = lane >> 4, pn = ctx - 1;
+  uint32_t vn[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt) vn[dt] = vnew[16 * dt + c];
 #pragma unroll
   for (int ps = 0; ps < C::PS; ++ps) {
     const int p0 = base + 32 * ps + 8 * g;
+    // per 32-bit word e2 (elements 2 e2, 2 e2 + 1): keep mask and new-value mask
+    uint32_t keep[4], put[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      const int pl = p0 + 2 * e2, ph = pl + 1;
+      keep[e2] = (pl < pn ? 0x0000ffffu : 0u) | (ph < pn ? 0xffff0000u : 0u);
+      put[e2] = (pl == pn ? 0x0000ffffu : 0u) | (ph == pn ? 0xffff0000u : 0u);
+    }
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
-      const uint32_t vn = vnew[16 * dt + c];
-      u32x4_t v = vf[ps][dt];
+      const uint32_t nv = vn[dt] | (vn[dt] << 16);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int p = p0 + e;
-        const uint32_t sh = (e & 1) * 16, keep = ~(0xffffu << sh);
-        uint32_t w = v[e >> 1];
-        w = (p == pn) ? ((w & keep) | (vn << sh)) : (p > pn ? (w & keep) : w);
-        v[e >> 1] = w;
-      }
-      vf[ps][dt] = v;
+      for (int e2 = 0; e2 < 4; ++e2) vf[ps][dt][e2] = (vf[ps][dt][e2] & keep[e2]) | (nv & put[e2]);
     }
   }
 }
@@ -162,7 +170,8 @@ TTS_DEV void dec_pv(float M, float& lsum, f32x4_t (&s)[DecShape<D, PW>::MT],
   for (int mt = 0; mt < C::MT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float p = (s[mt][r] == -INFINITY) ? 0.f : expf(s[mt][r] - M);
+      // (M is the finite context maximum: a masked score gives exp(-inf) = 0, no branch)
+      const float p = expf(s[mt][r] - M);
       lsum += p;
       s[mt][r] = p;
     }
@@ -283,7 +292,7 @@ TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, flo
                         u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
                         u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out) {
   dec_attend_w<D, PW, NW>(kc, vtc, S, ctx, scale, qs, knew, vnew, red, kf0, vf0, out,
-                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { __syncthreads(); });
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { lds_barrier(); });
 }
 
 // RoPE of one element (HF apply_rotary_pos_emb in bf16: x*cos + rotate_half(x)*sin, each

@@ -261,6 +261,27 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
 }
 
 // ------------------------------------------------------------------------ compute -----
+#ifdef TTS_STAMPS
+// diagnostic build only: per-workgroup clock stamps of the last launches (scripts/stamp_probe.py)
+static unsigned long long* g_stamps = nullptr;
+constexpr int kStampSlots = 1 << 16;
+static unsigned long long* stamp_buf() {
+  if (!g_stamps) {
+    HIP_CHECK(hipMalloc((void**)&g_stamps, kStampSlots * 8));
+    HIP_CHECK(hipMemset(g_stamps, 0, kStampSlots * 8));
+  }
+  return g_stamps;
+}
+extern "C" int tts_debug_stamps(unsigned long long* host, int n) {
+  if (!g_stamps || n > kStampSlots) return 1;
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpy(host, g_stamps, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  return hipMemset(g_stamps, 0, kStampSlots * 8) == hipSuccess ? 0 : 1;
+}
+#else
+static unsigned long long* stamp_buf() { return nullptr; }
+#endif
+
 namespace {
 
 // Decode attention of a one-row step fused into the QKV launch (lm_gemm_kernel.h,
@@ -343,6 +364,7 @@ struct Ctx {
       }
       a.x = xin; a.M = m; a.K = K; a.ldx = K;
       a.w = W; a.N = N;
+      a.stamps = stamp_buf();
       a.normw = normw; a.eps = c.rms_norm_eps;
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
@@ -372,6 +394,7 @@ struct Ctx {
     a.scale = (float)(1.0 / sqrt((double)D));
     a.q_rot = w.q_rot.as<bf16_t>(); a.out = w.attn_out.as<bf16_t>();
     a.blocks = w.blocks.as<int4>(); a.nblocks = w.nblocks;
+    a.stamps = stamp_buf();
     return a;
   }
 

@@ -59,6 +59,8 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   const size_t kvbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
   const bf16_t* kc = a.kcache + kvbase;
   const bf16_t* vtc = a.vtcache + kvbase;
+  unsigned long long* stp = wa.stamps ? wa.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  TTS_STAMP(stp, 0);
   u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
   if (wave * PW < ctx) {
     dec_load_k<D, PW>(kc, wave * PW, ctx, lane, kf);
@@ -88,7 +90,8 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     }
     raw[tid] = (uint32_t)v;
   }
-  __syncthreads();
+  lds_barrier();
+  TTS_STAMP(stp, 1);
   // RoPE of the group's q heads and of the new k (HF apply_rotary_pos_emb in bf16)
   if (tid < G * D) {
     const int g = tid / D;
@@ -98,9 +101,11 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     knew[d] = f2bf(rope_elem(rawb[G * D + d], rawb[G * D + (d < H2 ? d + H2 : d - H2)], d < H2, qc, qsn));
     vnew[d] = rawb[G * D + D + d];
   }
-  __syncthreads();
+  lds_barrier();
+  TTS_STAMP(stp, 2);
   dec_attend<D, PW, DEC_NW>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
                             a.out + (size_t)row * a.H * D + kvh * G * D);
+  TTS_STAMP(stp, 3);
   // the new position's roped k and v to the cache, after this workgroup's reads
   if (tid < D) {
     a.kcache[kvbase + (size_t)pos * D + tid] = knew[tid];
@@ -138,6 +143,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
   }
   constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
+  unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  TTS_STAMP(stp, 0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kpart = wave % KSPLIT;
@@ -313,7 +320,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           if (lane == 0 && c < achunks) red[c >> 6] = s;
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
 #pragma unroll
     for (int j = 0; j < EA; ++j) {
@@ -338,7 +345,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
    } else if (use_glds) {
     // rows landed by LDS-DMA: wait for this wave's DMA only (the weight ring issued after
     // it stays in flight), then every wave's (raw barrier: __syncthreads would drain the ring)
@@ -398,7 +405,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
     if constexpr (NORM) {
-      __syncthreads();
+      lds_barrier();
       for (int m = wave; m < M; m += WAVES) {
         bf16_t* xr = xs + (size_t)m * ldxs;
         float ss = 0.f;
@@ -422,10 +429,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
    }
   }
-
+  TTS_STAMP(stp, 1);
 
   // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
   float best_v[MT_MAX][4];
@@ -496,6 +503,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j);
     }
 
+    if (first) TTS_STAMP(stp, 2);
     if (a.diag & 2) {
       if (acc[0][0][0] == 1234.5f && a.out) a.out[0] = 0;
       continue;
@@ -515,7 +523,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
               for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
             }
       }
-      __syncthreads();
+      lds_barrier();
       if (kpart == 0) {
 #pragma unroll
         for (int p = 1; p < KSPLIT; ++p) {
@@ -530,7 +538,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
               }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
 
     // ---- epilogue (lane owns column n, rows m = mt*16 + 4*(lane>>4) + r)
@@ -577,6 +585,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
     }
+    if (first) TTS_STAMP(stp, 3);
     first = false;
     if constexpr (EPI == EPI_LOGITS) {
 #pragma unroll
@@ -601,7 +610,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     // across the unit-groups of the workgroup (only kpart==0 waves hold results)
     float* rv = red;
     int* ri = (int*)(red + UPW * MT_MAX * 16);
-    __syncthreads();
+    lds_barrier();
     if (kpart == 0 && (lane & 15) == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT_MAX; ++mt)
@@ -612,7 +621,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           ri[ugrp * MT_MAX * 16 + m] = best_i[mt][r];
         }
     }
-    __syncthreads();
+    lds_barrier();
     for (int m = threadIdx.x; m < M; m += NT) {
       float v = rv[m];
       int i = ri[m];

@@ -57,6 +57,7 @@ struct AttnArgs {
   bf16_t* out = nullptr;    // [rows][H*D] bf16 attention output
   const int4* blocks = nullptr;  // prefill: query blocks {first row, rows (<= 16), slot, first position}
   int nblocks = 0;
+  unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS)
 };
 
 struct WgemmArgs {
@@ -98,6 +99,7 @@ struct WgemmArgs {
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
   int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
+  unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS): [block][8]
   int csplit = 1;     // 2: each 16-column unit runs as two 8-column halves (twice the workgroups; filled in by launch_wgemm)
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
 };
