@@ -24,7 +24,8 @@ else:
     r = {k: round(m.bench_kernel(k, rows=1, ctx=450, iters=64)[0] * 1000, 2) for k in ks}
 print(json.dumps(r))
 '''
-runs = [("ctx", {})] + [("diag", {"TTS_WGEMM_DIAG": d}) for d in ("0", "1", "2", "3", "8")]
+runs = [("ctx", {})] + [("diag", {"TTS_WGEMM_DIAG": d}) for d in ("0", "1", "2", "3", "8")] + \
+    [("diag", {"TTS_STREAM_PLAN": "1"}), ("diag", {"TTS_CSPLIT": "0"})]
 for mode, extra in runs:
     env = dict(os.environ, **extra)
     out = subprocess.run([sys.executable, "-c", CHILD, ROOT, mode], env=env, capture_output=True, text=True, timeout=300)

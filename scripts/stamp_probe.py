@@ -36,9 +36,9 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn"):
         assert f(buf.ctypes.data, N) == 0
     t = buf.astype(np.int64)
     if k == "attention":
-        st = t[4096:4096 + 8 * 8].reshape(-1, 8)
+        st = t[16384:16384 + 8 * 8].reshape(-1, 8)
     else:
-        st = t[:4096].reshape(-1, 8)
+        st = t[:16384].reshape(-1, 32)
     st = st[st[:, 0] > 0]
     t0 = st[:, 0].min()
     us = (st - t0) / 100.0
@@ -47,9 +47,11 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn"):
     if k == "qkv_attn":
         proj, cons = us[:-8], us[-8:]  # (the attention workgroups are the grid's last 8)
         print(f"  projection  entry {q(proj[:, 0])}  prologue {q(proj[:, 1])}  streamed {q(proj[:, 2])}  epilogue {q(proj[:, 3])}")
-        print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  attended {q(cons[:, 3])}")
+        print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  max {q(cons[:, 5])}  pv {q(cons[:, 6])}  attended {q(cons[:, 3])}")
     elif k == "attention":
         print(f"  entry {q(us[:, 0])}  rope {q(us[:, 2])}  attended {q(us[:, 3])}")
     else:
         print(f"  entry {q(us[:, 0])}  prologue {q(us[:, 1])}  streamed {q(us[:, 2])}  epilogue {q(us[:, 3])}")
+        w = us[:, 8:24]
+        print(f"  waves streamed: first {q(np.nanmin(w, 1))} last {q(np.nanmax(w, 1))}  split-K barrier {q(us[:, 4])}  summed {q(us[:, 5])}")
     sys.stdout.flush()

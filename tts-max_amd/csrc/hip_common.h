@@ -15,8 +15,11 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 #ifdef TTS_STAMPS
 #define TTS_STAMP(buf, slot) \
   do { if ((buf) && threadIdx.x == 0) (buf)[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TTS_STAMP_WAVE(buf, slot) \
+  do { if ((buf) && (threadIdx.x & 63) == 0) (buf)[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define TTS_STAMP(buf, slot) do {} while (0)
+#define TTS_STAMP_WAVE(buf, slot) do {} while (0)
 #endif
 
 // bf16 -> fp32 is exact: the bf16 bits are the top half of the fp32 pattern.

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
   const size_t kvbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
   const bf16_t* kc = a.kcache + kvbase;
   const bf16_t* vtc = a.vtcache + kvbase;
-  unsigned long long* stp = a.stamps ? a.stamps + 4096 + (size_t)blockIdx.x * 8 : nullptr;
+  unsigned long long* stp = a.stamps ? a.stamps + 16384 + (size_t)blockIdx.x * 8 : nullptr;
   TTS_STAMP(stp, 0);
   // this wave's first-pass fragments before anything else (vmcnt retires in issue order)
   u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];

@@ -202,7 +202,7 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
                           const bf16_t* knew, const bf16_t* vnew, float* red,
                           u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
                           u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out, int wave,
-                          int tid, Bar bar) {
+                          int tid, Bar bar, unsigned long long* stp = nullptr) {
   using C = DecShape<D, PW>;
   const int lane = tid & 63;
   const int c = lane & 15, g = lane >> 4;
@@ -242,6 +242,7 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   if (lane < DEC_G) mred[wave * DEC_G + lane] = mx;
   bar();
+  TTS_STAMP(stp, 5);
   float M = -INFINITY;
 #pragma unroll
   for (int w = 0; w < NW; ++w) M = fmaxf(M, mred[w * DEC_G + (c & 3)]);
@@ -274,14 +275,19 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
     if (g == 0) lred[wave * DEC_G + c] = lsum;
   }
   bar();
+  TTS_STAMP(stp, 6);
   for (int i = tid; i < DEC_G * D; i += NW * 64) {
     const int h = i / D, d = i - h * D;
+    float v[NW];  // each group of reads in flight before its sums (wave order: deterministic)
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v[w] = lred[w * DEC_G + h];
     float O = 0.f, L = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {  // wave order: deterministic
-      O += ored[(w * DEC_G + h) * D + d];
-      L += lred[w * DEC_G + h];
-    }
+    for (int w = 0; w < NW; ++w) L += v[w];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v[w] = ored[(w * DEC_G + h) * D + d];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) O += v[w];
     out[h * D + d] = f2bf(O / L);
   }
 }
@@ -290,9 +296,10 @@ template <int D, int PW, int NW>
 TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, float scale, const float* qs,
                         const bf16_t* knew, const bf16_t* vnew, float* red,
                         u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
-                        u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out) {
+                        u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out,
+                        unsigned long long* stp = nullptr) {
   dec_attend_w<D, PW, NW>(kc, vtc, S, ctx, scale, qs, knew, vnew, red, kf0, vf0, out,
-                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { lds_barrier(); });
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { lds_barrier(); }, stp);
 }
 
 // RoPE of one element (HF apply_rotary_pos_emb in bf16: x*cos + rotate_half(x)*sin, each

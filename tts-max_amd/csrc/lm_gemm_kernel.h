@@ -59,7 +59,7 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   const size_t kvbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
   const bf16_t* kc = a.kcache + kvbase;
   const bf16_t* vtc = a.vtcache + kvbase;
-  unsigned long long* stp = wa.stamps ? wa.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  unsigned long long* stp = wa.stamps ? wa.stamps + (size_t)blockIdx.x * 32 : nullptr;
   TTS_STAMP(stp, 0);
   u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
   if (wave * PW < ctx) {
@@ -104,7 +104,7 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   lds_barrier();
   TTS_STAMP(stp, 2);
   dec_attend<D, PW, DEC_NW>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
-                            a.out + (size_t)row * a.H * D + kvh * G * D);
+                            a.out + (size_t)row * a.H * D + kvh * G * D, stp);
   TTS_STAMP(stp, 3);
   // the new position's roped k and v to the cache, after this workgroup's reads
   if (tid < D) {
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
   }
   constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
-  unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
   TTS_STAMP(stp, 0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j);
     }
 
-    if (first) TTS_STAMP(stp, 2);
+    if (first) { TTS_STAMP(stp, 2); TTS_STAMP_WAVE(stp, 8 + wave); }
     if (a.diag & 2) {
       if (acc[0][0][0] == 1234.5f && a.out) a.out[0] = 0;
       continue;
@@ -512,32 +512,49 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     if constexpr (KSPLIT > 1) {
       // slot of wave (ugrp, kpart > 0): ugrp * (KSPLIT-1) + kpart - 1
       constexpr int PS = NG * MT_MAX * 4 * 64;
+      // one 16-B LDS access per (tile, lane): the sums (fixed order, p ascending) are the
+      // same as element-wise, and the KSPLIT - 1 reads of a lane are all in flight at once
       if (kpart > 0) {
         float* myred = red + (size_t)(ugrp * (KSPLIT - 1) + kpart - 1) * PS;
 #pragma unroll
         for (int g = 0; g < NG; ++g)
 #pragma unroll
           for (int mt = 0; mt < MT_MAX; ++mt)
-            if (mt < mtn) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) myred[((g * MT_MAX + mt) * 4 + r) * 64 + lane] = acc[g][mt][r];
-            }
+            if (MT_MAX == 1 || mt < mtn) *(f32x4_t*)(myred + ((g * MT_MAX + mt) * 64 + lane) * 4) = acc[g][mt];
       }
       lds_barrier();
+      if (first) TTS_STAMP(stp, 4);
       if (kpart == 0) {
+        constexpr int NPV = (KSPLIT - 1) * NG * MT_MAX;
+        if constexpr (NPV <= 16) {  // every partial read issued before the first add
+          f32x4_t pv[KSPLIT > 1 ? KSPLIT - 1 : 1][NG][MT_MAX];
 #pragma unroll
-        for (int p = 1; p < KSPLIT; ++p) {
-          const float* o = red + (size_t)(ugrp * (KSPLIT - 1) + p - 1) * PS;
+          for (int p = 1; p < KSPLIT; ++p)
 #pragma unroll
-          for (int g = 0; g < NG; ++g)
+            for (int g = 0; g < NG; ++g)
 #pragma unroll
-            for (int mt = 0; mt < MT_MAX; ++mt)
-              if (mt < mtn) {
+              for (int mt = 0; mt < MT_MAX; ++mt)
+                pv[p - 1][g][mt] = *(const f32x4_t*)(red + (size_t)(ugrp * (KSPLIT - 1) + p - 1) * PS +
+                                                     ((g * MT_MAX + mt) * 64 + lane) * 4);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[g][mt][r] += o[((g * MT_MAX + mt) * 4 + r) * 64 + lane];
-              }
+          for (int p = 1; p < KSPLIT; ++p)
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+#pragma unroll
+              for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] += pv[p - 1][g][mt];
+        } else {
+#pragma unroll
+          for (int p = 1; p < KSPLIT; ++p) {
+            const float* o = red + (size_t)(ugrp * (KSPLIT - 1) + p - 1) * PS;
+#pragma unroll
+            for (int g = 0; g < NG; ++g)
+#pragma unroll
+              for (int mt = 0; mt < MT_MAX; ++mt)
+                if (mt < mtn) acc[g][mt] += *(const f32x4_t*)(o + ((g * MT_MAX + mt) * 64 + lane) * 4);
+          }
         }
       }
+      if (first) TTS_STAMP(stp, 5);
       lds_barrier();
     }
 
