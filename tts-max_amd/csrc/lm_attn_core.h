@@ -170,8 +170,10 @@ TTS_DEV void dec_pv(float M, float& lsum, f32x4_t (&s)[DecShape<D, PW>::MT],
   for (int mt = 0; mt < C::MT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      // (M is the finite context maximum: a masked score gives exp(-inf) = 0, no branch)
-      const float p = expf(s[mt][r] - M);
+      // exp as the hardware 2^x of (s - M) log2 e, as FlashAttention's kernels evaluate it (one
+      // v_exp_f32; the libm expf is a ~20-instruction range reduction).  M is the finite
+      // context maximum: a masked score gives 2^-inf = 0, no branch.
+      const float p = __builtin_amdgcn_exp2f((s[mt][r] - M) * 1.44269504088896341f);
       lsum += p;
       s[mt][r] = p;
     }
