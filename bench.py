@@ -197,16 +197,21 @@ def main():
     for k in lm.KERNELS:
         ms, by = lm.bench_kernel(k, rows=B, ctx=ctx_mid, iters=args.kernel_iters)
         kern[k] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
-    # the one-row step runs QKV with the attention fused in (one launch for both)
-    fused = False
+    # the one-row step runs QKV with the attention fused in (one launch for both), and with
+    # o_proj fused behind the attention where that fits (TTS_FUSED_OPROJ, default on)
+    fused, fused_o = False, False
     try:
         ms, by = lm.bench_kernel("qkv_attn", rows=B, ctx=ctx_mid, iters=args.kernel_iters)
         kern["qkv_attn"] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
         fused = True
+        ms, by = lm.bench_kernel("qkv_attn_oproj", rows=B, ctx=ctx_mid, iters=args.kernel_iters)
+        kern["qkv_attn_oproj"] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
+        fused_o = True
     except Exception:  # noqa: BLE001 (not this shape: separate launches)
         pass
     # per-step share: the layer kernels once per layer, lm_head once
-    in_step = [k for k in kern if not (fused and k in ("qkv", "attention"))]
+    in_step = [k for k in kern if not (fused and k in ("qkv", "attention"))
+               and not (fused_o and k in ("qkv_attn", "o_proj"))]
     share = {k: kern[k]["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k in in_step}
     dom = max(share, key=share.get)
     step_ms = lm_decode / max(dec_steps, 1)

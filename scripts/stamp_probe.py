@@ -30,7 +30,7 @@ def q(v):
     return "/".join(f"{x:5.2f}" for x in (np.min(v), np.median(v), np.max(v)))
 
 
-for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn"):
+for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn_oproj"):
     for rep in range(3):
         m.bench_kernel(k, rows=1, ctx=ctx, iters=1)
         assert f(buf.ctypes.data, N) == 0
@@ -44,7 +44,7 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn"):
     us = (st - t0) / 100.0
     us[st == 0] = np.nan
     print(f"{k} ctx={ctx}: {len(st)} workgroups (min/median/max us from first entry)")
-    if k == "qkv_attn":
+    if k in ("qkv_attn", "qkv_attn_oproj"):
         proj, cons = us[:-8], us[-8:]  # (the attention workgroups are the grid's last 8)
         print(f"  projection  entry {q(proj[:, 0])}  prologue {q(proj[:, 1])}  streamed {q(proj[:, 2])}  epilogue {q(proj[:, 3])}")
         print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  max {q(cons[:, 5])}  pv {q(cons[:, 6])}  attended {q(cons[:, 3])}")

@@ -204,7 +204,8 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
                           const bf16_t* knew, const bf16_t* vnew, float* red,
                           u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
                           u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out, int wave,
-                          int tid, Bar bar, unsigned long long* stp = nullptr) {
+                          int tid, Bar bar, unsigned long long* stp = nullptr, uint64_t* gout = nullptr,
+                          uint32_t gtag = 0) {
   using C = DecShape<D, PW>;
   const int lane = tid & 63;
   const int c = lane & 15, g = lane >> 4;
@@ -290,7 +291,14 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
     for (int w = 0; w < NW; ++w) v[w] = ored[(w * DEC_G + h) * D + d];
 #pragma unroll
     for (int w = 0; w < NW; ++w) O += v[w];
-    out[h * D + d] = f2bf(O / L);
+    const bf16_t ob = f2bf(O / L);
+    out[h * D + d] = ob;
+    if (gout) {  // (whole waves: DEC_G * D is a multiple of 64) pairs (d, d + 1) as one granule
+      const uint32_t other = (uint32_t)__shfl_xor((int)ob, 1, 64);
+      if (!(d & 1))
+        __hip_atomic_store(gout + (h * D + d) / 2, ((uint64_t)gtag << 32) | (other << 16) | (uint32_t)ob,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -299,9 +307,10 @@ TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, flo
                         const bf16_t* knew, const bf16_t* vnew, float* red,
                         u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
                         u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out,
-                        unsigned long long* stp = nullptr) {
+                        unsigned long long* stp = nullptr, uint64_t* gout = nullptr, uint32_t gtag = 0) {
   dec_attend_w<D, PW, NW>(kc, vtc, S, ctx, scale, qs, knew, vnew, red, kf0, vf0, out,
-                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { lds_barrier(); }, stp);
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { lds_barrier(); }, stp,
+                          gout, gtag);
 }
 
 // RoPE of one element (HF apply_rotary_pos_emb in bf16: x*cos + rotate_half(x)*sin, each

@@ -236,7 +236,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.act.alloc((size_t)R * FF * 2);
   w.last_x.alloc((size_t)B * HID * 2);
   w.blocks.alloc(((size_t)R / 16 + B + 1) * 16);  // prefill query blocks: <= rows/16 + one per sequence
-  w.gran.alloc((size_t)QKV / 2 * 8);
+  w.gran.alloc((size_t)(QKV + H * D) / 2 * 8);  // q|k|v granules, then the attention row's
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
@@ -288,6 +288,12 @@ namespace {
 // fattn_consumer): default on; TTS_FUSED_ATTN=0 keeps the separate attention launch.
 bool use_fused_attn() {
   static const bool v = !(getenv("TTS_FUSED_ATTN") && !atoi(getenv("TTS_FUSED_ATTN")));
+  return v;
+}
+// ... and o_proj fused behind that attention (lm_gemm_kernel.h fused_oproj): default on;
+// TTS_FUSED_OPROJ=0 keeps the separate o_proj launch.
+bool use_fused_oproj() {
+  static const bool v = !(getenv("TTS_FUSED_OPROJ") && !atoi(getenv("TTS_FUSED_OPROJ")));
   return v;
 }
 
@@ -405,14 +411,35 @@ struct Ctx {
            c.num_layers >= 2 && c.num_layers <= 64 &&
            wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
   }
-  WgemmArgs fused_attn_args(const AttnArgs& a, int layer) {
+  WgemmArgs fused_attn_args(const AttnArgs& a, int layer, bool with_oproj = false) {
     WgemmArgs fx;
     fx.gran = w.gran.as<uint64_t>();
     fx.fa = a;
     fx.fattn_wgs = a.rows * a.KVH;
     fx.fattn_layer = layer;
     fx.fattn_err = w.ferr.as<int>();
+    if (with_oproj) {
+      const LmLayer& ly = M.layers[layer];
+      const WgemmPlan po = plan_wgemm(1, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu);
+      fx.fo_w = ly.wo;
+      fx.fo_units = c.hidden_size / 16;
+      fx.fo_ur = po.sp.ur();
+      fx.fo_resid = w.x.as<bf16_t>();
+    }
     return fx;
+  }
+  // o_proj can ride the fused QKV + attention launch: its stream plan has the launch's shape
+  // (16 waves, 2-tile stages, K split 16 ways, one K chunk, two stages = the ring), one round
+  // of units, at most one unit per projection workgroup, 128 K values per wave
+  bool fused_oproj_ok() const {
+    if (!use_fused_oproj()) return false;
+    const int HD = c.num_heads * c.head_dim, HID = c.hidden_size;
+    const WgemmPlan pq = plan_wgemm(1, QKV(), HID, EPI_STORE, e->num_cu);
+    const WgemmPlan po = plan_wgemm(1, HID, HD, EPI_RESID, e->num_cu);
+    const StreamPlan& s = po.sp;
+    return s.waves == 16 && s.ku == 2 && s.ksplit == 16 && s.kc == 1 && s.ng == 1 && HD == 16 * 128 &&
+           (HD / 32) / (s.ksplit * s.ku) == 2 && HID / 16 <= s.ur() && HID / 16 <= pq.sp.grid &&
+           pq.sp.waves == 16 && pq.sp.ku == 2 && pq.sp.ksplit == 16;
   }
 
   // One transformer stack pass over `rows` rows held in w.x.
@@ -420,11 +447,12 @@ struct Ctx {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
+    const bool foproj = fattn && fused_oproj_ok();
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
       if (fattn) {
-        const WgemmArgs fx = fused_attn_args(a, l);
+        const WgemmArgs fx = fused_attn_args(a, l, foproj);
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE, &fx);
       } else {
@@ -440,7 +468,8 @@ struct Ctx {
         launch_rope_append(a, s);
         launch_attn_prefill(a, s);
       }
-      gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID);
+      if (!foproj)
+        gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
@@ -929,8 +958,9 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 6 && iters >= 1, "bad kernel selector");
-  TTS_REQUIRE(which != 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
+  TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which < 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
+  TTS_REQUIRE(which != 7 || Ctx(e, e->stream).fused_oproj_ok(), "fused o_proj is off or does not fit");
   hipStream_t s = e->stream;
   Ctx X(e, s);
   const tts_lm_config& c = X.c;
@@ -994,13 +1024,15 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         launch_attn_decode_step(aa, s);
         b = (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2 + act_rw * QKV;
         break;
-      case 6: {  // QKV with the decode attention fused in (the one-row decode step's form)
+      case 6:
+      case 7: {  // QKV with the decode attention fused in (the one-row decode step's form), + o_proj (7)
         const AttnArgs al = X.attn_args(li, rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
-        const WgemmArgs fx = X.fused_attn_args(al, li);
+        const WgemmArgs fx = X.fused_attn_args(al, li, which == 7);
         X.gemm(e->w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV, ly.ln1, e->w.qkv.as<bf16_t>(), QKV, nullptr,
                EPI_STORE, &fx);
         b = 2.0 * QKV * HID + act_rw * (HID + QKV) + 2.0 * HID +
             (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2;
+        if (which == 7) b += 2.0 * HID * HD + act_rw * (HD + 2 * HID);
         break;
       }
     }

@@ -104,12 +104,79 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   lds_barrier();
   TTS_STAMP(stp, 2);
   dec_attend<D, PW, DEC_NW>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
-                            a.out + (size_t)row * a.H * D + kvh * G * D, stp);
+                            a.out + (size_t)row * a.H * D + kvh * G * D, stp,
+                            wa.fo_units ? wa.gran + wa.N / 2 + kvh * G * D / 2 : nullptr, tag);
   TTS_STAMP(stp, 3);
   // the new position's roped k and v to the cache, after this workgroup's reads
   if (tid < D) {
     a.kcache[kvbase + (size_t)pos * D + tid] = knew[tid];
     a.vtcache[kvbase + (size_t)tid * a.max_seq + pos] = vnew[tid];
+  }
+}
+
+TTS_DEV bf16x8_t as_bf16x8(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+// ------------------------------------------- o_proj fused behind the attention -----
+// Projection workgroup u (< fo_units) of the one-row QKV + attention launch, after its QKV
+// unit: o_proj unit u (16 output columns, K = H*D split over the 16 waves as in the o_proj
+// launch, whose stream plan has the same shape, so the tiles, the split-K order and the
+// residual epilogue are the o_proj launch's: same bits).  Its weight stages are issued first
+// and land while the attention runs; then each wave waits for the 64 granules of its K range
+// (one per lane: the attention row of kv group kpart / 2), stages them in LDS and multiplies.
+template <int KU, int KSPLIT, int R>
+TTS_DEV void fused_oproj(const WgemmArgs& a, bf16_t* xs, float* red, int wave, int lane, uint32_t tag) {
+  const int kpart = wave % KSPLIT;
+  const int u = blockIdx.x;
+  const int nr = min(a.fo_ur, a.fo_units);
+  u32x4_t wr[R][KU];
+#pragma unroll
+  for (int st = 0; st < R; ++st)
+#pragma unroll
+    for (int kk = 0; kk < KU; ++kk)
+      wr[st][kk] = __builtin_nontemporal_load((const u32x4_t*)a.fo_w +
+                                              ((((long long)st * nr + u) * KSPLIT + kpart) * KU + kk) * 64 + lane);
+  const bf16_t rr = a.fo_resid[u * 16 + (lane & 15)];
+  const uint64_t* g = a.gran + a.N / 2 + kpart * 64 + lane;
+  uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int spins = 0;
+  while (!__all((uint32_t)(v >> 32) == tag)) {
+    if (++spins > FATTN_MAX_SPINS) {
+      if (lane == 0) __hip_atomic_store(a.fattn_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // this wave's 128 attention values into its own K range of the LDS row (read back by this
+  // wave only: LDS operations of one wave complete in order)
+  *(uint32_t*)(xs + kpart * 128 + 2 * lane) = (uint32_t)v;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const int akoff = 8 * (lane >> 4);
+#pragma unroll
+  for (int st = 0; st < R; ++st)
+#pragma unroll
+    for (int kk = 0; kk < KU; ++kk) {
+      const int k = ((kpart * R + st) * KU + kk) * 32 + akoff;
+      const u32x4_t av = *(const u32x4_t*)(xs + k);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av), as_bf16x8(wr[st][kk]), acc, 0, 0, 0);
+    }
+  // split-K combine (as the GEMM kernel's: 16-B partials, p ascending), residual epilogue
+  if (kpart > 0) *(f32x4_t*)(red + ((size_t)(kpart - 1) * 64 + lane) * 4) = acc;
+  lds_barrier();
+  if (kpart == 0) {
+    constexpr int HB = 8;  // reads in flight per batch (register budget of the 16-wave launch)
+#pragma unroll
+    for (int p0 = 1; p0 < KSPLIT; p0 += HB) {
+      f32x4_t pv[HB];
+#pragma unroll
+      for (int j = 0; j < HB; ++j)
+        if (p0 + j < KSPLIT) pv[j] = *(const f32x4_t*)(red + ((size_t)(p0 + j - 1) * 64 + lane) * 4);
+#pragma unroll
+      for (int j = 0; j < HB; ++j)
+        if (p0 + j < KSPLIT) acc += pv[j];
+    }
+    if (lane < 16) a.fo_resid[u * 16 + lane] = f2bf(bf2f(rr) + rbf(acc[0]));
   }
 }
 
@@ -120,7 +187,6 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
 // of KU tiles (KU KiB), double-buffered, and the stream never stops: the first stage is
 // issued before the A-operand prologue (RMSNorm / attention combine), and the last stage
 // of a unit prefetches the first stage of the wave's next unit.
-TTS_DEV bf16x8_t as_bf16x8(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 // Better (value, index): larger value wins, lower index on ties (torch.argmax semantics).
 TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
@@ -612,6 +678,12 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
   }
 
+  if constexpr (FATT) {
+    if (a.fattn_wgs && a.fo_units > 0 && (int)blockIdx.x < a.fo_units) {
+      lds_barrier();  // (every wave past the QKV unit's LDS use)
+      fused_oproj<KU, KSPLIT, R>(a, xs, red, wave, lane, ftag);
+    }
+  }
   if constexpr (EPI == EPI_LOGITS) {
     // lanes sharing (lane >> 4) hold the same rows: butterfly over the 16 columns
 #pragma unroll
@@ -674,6 +746,12 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
           a.gran && a.fattn_err && !a.sliced))
       throw std::runtime_error("wgemm: fused attention needs the one-row 16-wave QKV launch (D 64)");
     if (!EARLY) throw std::runtime_error("wgemm: fused attention needs the register-staged prologue");
+    if (a.fo_units) {  // fused o_proj: one unit per projection workgroup, one granule per lane
+      const int S = (a.fa.H * a.fa.D / 32) / (KSPLIT * KU);
+      if (!(a.fo_w && a.fo_resid && a.fo_units <= grid && a.fo_units <= a.fo_ur && S == R &&
+            a.fa.H * a.fa.D == KSPLIT * 128 && KSPLIT == WAVES))
+        throw std::runtime_error("wgemm: fused o_proj shape mismatch");
+    }
     lds = std::max(lds, fattn_lds_bytes());
     grid += a.fattn_wgs;
     // The appended consumers spin on the projection workgroups' granules: every workgroup of

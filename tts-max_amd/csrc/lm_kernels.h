@@ -99,6 +99,14 @@ struct WgemmArgs {
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
   int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
+  // o_proj fused behind the attention (fo_units > 0): the attention workgroups also publish
+  // the bf16 attention row as granules (gran + N/2, same tag); projection workgroup b <
+  // fo_units then computes o_proj unit b (tiled weights fo_w, layout rounds fo_ur, one round)
+  // with the residual epilogue on fo_resid (the hidden row), its o_proj weights loaded while
+  // the attention runs
+  const bf16_t* fo_w = nullptr;
+  int fo_units = 0, fo_ur = 0;
+  bf16_t* fo_resid = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS): [block][8]
   int csplit = 1;     // 2: each 16-column unit runs as two 8-column halves (twice the workgroups; filled in by launch_wgemm)
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream

@@ -331,8 +331,9 @@ class MI355XSpeechLM:
     def bench_kernel(self, which: str, rows: int = 1, ctx: int = 450, iters: int = 50) -> tuple[float, float]:
         """(avg ms per launch, algorithmic bytes per launch) of one decode-step kernel."""
         ms, b = ctypes.c_float(), ctypes.c_double()
-        # qkv_attn: QKV with the decode attention fused in (the one-row step's form)
-        sel = {"qkv_attn": 6}.get(which)
+        # qkv_attn: QKV with the decode attention fused in (the one-row step's form);
+        # qkv_attn_oproj: the same launch also carrying o_proj (the default one-row step)
+        sel = {"qkv_attn": 6, "qkv_attn_oproj": 7}.get(which)
         sel = self.KERNELS.index(which) if sel is None else sel
         _lib.check(self._lib.tts_lm_bench_kernel(self._h, sel, rows, ctx, iters,
                                                  ctypes.byref(ms), ctypes.byref(b)))
