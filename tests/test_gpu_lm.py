@@ -273,24 +273,25 @@ print(json.dumps(new))
 def test_fused_qkv_attention_equals_separate_launches():
     """The one-row decode step's QKV launch with the attention fused in (q/k/v handed to
     appended attention workgroups as tagged granules, lm_gemm_kernel.h fattn_consumer) and
-    the separate chunked attention launch (TTS_FUSED_ATTN=0) produce the same greedy ids on
-    TTS-1 over 1.2k generated positions: 11 chunks of 128, so workgroups of the fused launch
-    also take a second chunk (chunk slots 0..2 of 8) and the new position crosses every
-    chunk boundary."""
+    o_proj fused behind that attention (the attention row handed back to the projection
+    workgroups as granules, fused_oproj), the same launch without o_proj
+    (TTS_FUSED_OPROJ=0), and all-separate launches (TTS_FUSED_ATTN=0) produce the same greedy
+    ids on TTS-1 over 1.2k generated positions: the context crosses the 1,024 positions of the
+    attention's first pass (a second pass per wave) and every 64-position wave boundary."""
     import json
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    for v in ("1", "0"):
-        env = dict(os.environ, TTS_FUSED_ATTN=v)
+    for fa, fo in (("1", "1"), ("1", "0"), ("0", "0")):
+        env = dict(os.environ, TTS_FUSED_ATTN=fa, TTS_FUSED_OPROJ=fo)
         r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, root], env=env, capture_output=True, text=True,
                            timeout=110)
         assert r.returncode == 0, r.stderr[-2000:]
-        outs[v] = json.loads(r.stdout.strip().splitlines()[-1])
-    assert len(outs["1"]) == 1400 - 202
-    assert outs["1"] == outs["0"]
+        outs[fa + fo] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(outs["11"]) == 1400 - 202
+    assert outs["11"] == outs["10"] == outs["00"]
 
 
 @pytest.mark.parametrize("rows", [1, 8])
