@@ -279,6 +279,7 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
   }
   bar();
   TTS_STAMP(stp, 6);
+  bf16_t gob = 0;  // (granule output: this thread's element, i == tid: one iteration)
   for (int i = tid; i < DEC_G * D; i += NW * 64) {
     const int h = i / D, d = i - h * D;
     float v[NW];  // each group of reads in flight before its sums (wave order: deterministic)
@@ -293,12 +294,15 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
     for (int w = 0; w < NW; ++w) O += v[w];
     const bf16_t ob = f2bf(O / L);
     out[h * D + d] = ob;
-    if (gout) {  // (whole waves: DEC_G * D is a multiple of 64) pairs (d, d + 1) as one granule
-      const uint32_t other = (uint32_t)__shfl_xor((int)ob, 1, 64);
-      if (!(d & 1))
-        __hip_atomic_store(gout + (h * D + d) / 2, ((uint64_t)gtag << 32) | (other << 16) | (uint32_t)ob,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (gout) gob = ob;
+  }
+  if (gout) {  // the row as granules: pairs (d, d + 1) through LDS (the partials are read)
+    bar();
+    if (tid < DEC_G * D) ((bf16_t*)ored)[tid] = gob;
+    bar();
+    if (tid < DEC_G * D / 2)
+      __hip_atomic_store(gout + tid, ((uint64_t)gtag << 32) | ((const uint32_t*)ored)[tid], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
