@@ -275,8 +275,8 @@ def test_fused_qkv_attention_equals_separate_launches():
     appended attention workgroups as tagged granules, lm_gemm_kernel.h fattn_consumer) and
     o_proj fused behind that attention (the attention row handed back to the projection
     workgroups as granules, fused_oproj), the same launch without o_proj
-    (TTS_FUSED_OPROJ=0), and all-separate launches (TTS_FUSED_ATTN=0) produce the same greedy
-    ids on TTS-1 over 1.2k generated positions: the context crosses the 1,024 positions of the
+    (TTS_FUSED_OPROJ=0), and all-separate launches (TTS_FUSED_ATTN=0) produce the same greedy ids on
+    TTS-1 over 1.2k generated positions: the context crosses the 1,024 positions of the
     attention's first pass (a second pass per wave) and every 64-position wave boundary."""
     import json
     import subprocess

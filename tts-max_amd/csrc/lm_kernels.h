@@ -60,6 +60,25 @@ struct AttnArgs {
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS)
 };
 
+// ---- sampling / bookkeeping state of a decode step (lm_ops.hip, lm_finalize.h)
+struct StepState {
+  int* tokens;        // [B] token fed to the next step
+  int* pos;           // [B] position of the next token (= current length)
+  int* gen_count;     // [B] tokens generated so far
+  int* limit;         // [B] max new tokens
+  int* done;          // [B]
+  int* eos_mask;      // [B] eos id while gen_count < min_new, else -1
+  uint32_t* seen;     // [B][seen_stride]
+  int seen_stride;
+  int* out_ids;       // [B][out_stride]
+  int out_stride;
+  int* n_active;      // [1]
+  uint16_t* counts;   // [B][V] new-token counts (frequency penalty) or nullptr
+  unsigned long long* row_seed;  // [B] sampling key of each row
+  int eos_id;
+  int min_new;
+};
+
 struct WgemmArgs {
   const bf16_t* x = nullptr;  // A: [M][ldx] bf16 activations
   int M = 0, K = 0, ldx = 0;
@@ -199,24 +218,6 @@ struct SampleArgs {
 constexpr int SAMPLE_MAX_TOP_K = 1024;
 void launch_sample(const SampleArgs& a, int B, hipStream_t s);
 
-// ---- sampling / bookkeeping (lm_ops.hip)
-struct StepState {
-  int* tokens;        // [B] token fed to the next step
-  int* pos;           // [B] position of the next token (= current length)
-  int* gen_count;     // [B] tokens generated so far
-  int* limit;         // [B] max new tokens
-  int* done;          // [B]
-  int* eos_mask;      // [B] eos id while gen_count < min_new, else -1
-  uint32_t* seen;     // [B][seen_stride]
-  int seen_stride;
-  int* out_ids;       // [B][out_stride]
-  int out_stride;
-  int* n_active;      // [1]
-  uint16_t* counts;   // [B][V] new-token counts (frequency penalty) or nullptr
-  unsigned long long* row_seed;  // [B] sampling key of each row
-  int eos_id;
-  int min_new;
-};
 void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
                             int nparts, StepState st, int B, const bf16_t* embed, bf16_t* x,
                             int hidden, hipStream_t s);

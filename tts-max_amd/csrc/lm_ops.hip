@@ -3,6 +3,7 @@
 // and the deterministic synthetic-weight generator shared with tts_amd/synth.py.
 #include "hip_common.h"
 #include "lm_kernels.h"
+#include "lm_finalize.h"
 
 namespace tts {
 
@@ -116,61 +117,15 @@ void launch_gather_rows(const bf16_t* x, int ld, const int* rows, bf16_t* y, int
 }
 
 // --------------------------------------------------------------- greedy finalize -------
-// One workgroup per sequence: reduce the lm_head partial argmaxes (lowest index on ties),
-// append the token, update the repetition-penalty id set, stop on EOS / length, and gather
-// the next step's input embedding.
+// One workgroup per sequence (lm_finalize.h finalize_row).
 __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
                                        int part_stride, int nparts, StepState st,
                                        const bf16_t* __restrict__ embed, bf16_t* __restrict__ x,
                                        int hidden) {
-  __shared__ float sv[4];
-  __shared__ int si[4];
-  __shared__ int stok;
+  __shared__ int lds[16];
   const int b = blockIdx.x;
-  // the row's state is read with the partials (one round trip), not after the reduction
-  const int done = st.done[b];
-  int g0 = 0, lim = 0, pos0 = 0;
-  if (threadIdx.x == 0) { g0 = st.gen_count[b]; lim = st.limit[b]; pos0 = st.pos[b]; }
-  float v = -INFINITY;
-  int i = 0x7fffffff;
-  for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
-    const float v2 = pv[(size_t)b * part_stride + p];
-    const int i2 = pi[(size_t)b * part_stride + p];
-    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
-  }
-  if (done) return;  // (uniform)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float v2 = __shfl_xor(v, o, 64);
-    const int i2 = __shfl_xor(i, o, 64);
-    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
-  }
-  if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; si[threadIdx.x >> 6] = i; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
-      if (sv[w] > v || (sv[w] == v && si[w] < i)) { v = sv[w]; i = si[w]; }
-    // all-(-inf) rows cannot happen (only EOS is masked); guard anyway
-    const int tok = (i == 0x7fffffff) ? 0 : i;
-    const int g = g0;
-    st.out_ids[(size_t)b * st.out_stride + g] = tok;
-    st.gen_count[b] = g + 1;
-    st.seen[(size_t)b * st.seen_stride + (tok >> 5)] |= 1u << (tok & 31);
-    if (st.counts) st.counts[(size_t)b * st.seen_stride * 32 + tok] += 1;
-    st.tokens[b] = tok;
-    st.pos[b] = pos0 + 1;
-    const bool stop = (tok == st.eos_id) || (g + 1 >= lim);
-    st.eos_mask[b] = (g + 1 < st.min_new) ? st.eos_id : -1;
-    if (stop) {
-      st.done[b] = 1;
-      atomicSub(st.n_active, 1);
-    }
-    stok = tok;
-  }
-  __syncthreads();
-  const u32x4_t* src = (const u32x4_t*)(embed + (size_t)stok * hidden);
-  u32x4_t* dst = (u32x4_t*)(x + (size_t)b * hidden);
-  for (int k = threadIdx.x; k < hidden / 8; k += blockDim.x) dst[k] = src[k];
+  finalize_row<256, false>(pv + (size_t)b * part_stride, pi + (size_t)b * part_stride, nparts, st, b, embed, x,
+                           hidden, lds);
 }
 
 void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
