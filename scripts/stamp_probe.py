@@ -45,7 +45,8 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn
     us[st == 0] = np.nan
     print(f"{k} ctx={ctx}: {len(st)} workgroups (min/median/max us from first entry)")
     if k in ("qkv_attn", "qkv_attn_oproj"):
-        proj, cons = us[:-8], us[-8:]  # (the attention workgroups are the grid's last 8)
+        first = os.environ.get("TTS_FATTN_FIRST", "1") != "0"  # the attention workgroups: first or last 8
+        proj, cons = (us[8:], us[:8]) if first else (us[:-8], us[-8:])
         print(f"  projection  entry {q(proj[:, 0])}  prologue {q(proj[:, 1])}  streamed {q(proj[:, 2])}  epilogue {q(proj[:, 3])}")
         print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  max {q(cons[:, 5])}  pv {q(cons[:, 6])}  attended {q(cons[:, 3])}")
     elif k == "attention":

@@ -418,6 +418,8 @@ struct Ctx {
     fx.fattn_wgs = a.rows * a.KVH;
     fx.fattn_layer = layer;
     fx.fattn_err = w.ferr.as<int>();
+    static const bool first = !(getenv("TTS_FATTN_FIRST") && !atoi(getenv("TTS_FATTN_FIRST")));
+    fx.fattn_first = first ? 1 : 0;
     if (with_oproj) {
       const LmLayer& ly = M.layers[layer];
       const WgemmPlan po = plan_wgemm(1, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu);

@@ -124,9 +124,8 @@ TTS_DEV bf16x8_t as_bf16x8(u32x4_t v) { return __builtin_bit_cast(bf16x8_t, v); 
 // and land while the attention runs; then each wave waits for the 64 granules of its K range
 // (one per lane: the attention row of kv group kpart / 2), stages them in LDS and multiplies.
 template <int KU, int KSPLIT, int R>
-TTS_DEV void fused_oproj(const WgemmArgs& a, bf16_t* xs, float* red, int wave, int lane, uint32_t tag) {
+TTS_DEV void fused_oproj(const WgemmArgs& a, bf16_t* xs, float* red, int wave, int lane, uint32_t tag, int u) {
   const int kpart = wave % KSPLIT;
-  const int u = blockIdx.x;
   const int nr = min(a.fo_ur, a.fo_units);
   u32x4_t wr[R][KU];
 #pragma unroll
@@ -203,12 +202,17 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   constexpr int NT = WAVES * 64;
   constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && NORM && EARLY && WAVES == DEC_NW;
   if constexpr (FATT) {
-    if (a.fattn_wgs && (int)blockIdx.x >= (int)gridDim.x - a.fattn_wgs) {
-      fattn_consumer<NT>(a, smem, blockIdx.x - (gridDim.x - a.fattn_wgs));
+    // the attention workgroups: the grid's first fattn_wgs blocks (fattn_first: dispatched
+    // first, their K / V loads ahead of the projection's weight stream) or its last ones
+    const int cb = a.fattn_first ? (int)blockIdx.x : (int)blockIdx.x - ((int)gridDim.x - a.fattn_wgs);
+    if (a.fattn_wgs && cb >= 0 && cb < a.fattn_wgs) {
+      fattn_consumer<NT>(a, smem, cb);
       return;
     }
   }
   constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
+  // this workgroup's index among the GEMM workgroups (the attention ones excluded)
+  const int bx = (FATT && a.fattn_wgs && a.fattn_first) ? (int)blockIdx.x - a.fattn_wgs : (int)blockIdx.x;
   unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
   TTS_STAMP(stp, 0);
   const int lane = threadIdx.x & 63;
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
   }
   // (c) epilogue operands of the wave's first unit: residual values / EOS mask + seen bits
-  int u = blockIdx.x * UPW + ugrp;
+  int u = bx * UPW + ugrp;
   const int u_first = min(u, units - 1);
   bf16_t rre[MT_MAX][4];
   int eosr[MT_MAX][4];
@@ -509,7 +513,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     for (int r = 0; r < 4; ++r) { best_v[mt][r] = -INFINITY; best_i[mt][r] = 0x7fffffff; }
 
   bool first = true;
-  for (int ubase = blockIdx.x * UPW; ubase < units; ubase += ustride) {
+  for (int ubase = bx * UPW; ubase < units; ubase += ustride) {
     u = ubase + ugrp;
     const bool active = u < units;
     uint32_t seen_nxt[MT_MAX][4];
@@ -679,9 +683,9 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   }
 
   if constexpr (FATT) {
-    if (a.fattn_wgs && a.fo_units > 0 && (int)blockIdx.x < a.fo_units) {
+    if (a.fattn_wgs && a.fo_units > 0 && bx < a.fo_units) {
       lds_barrier();  // (every wave past the QKV unit's LDS use)
-      fused_oproj<KU, KSPLIT, R>(a, xs, red, wave, lane, ftag);
+      fused_oproj<KU, KSPLIT, R>(a, xs, red, wave, lane, ftag, bx);
     }
   }
   if constexpr (EPI == EPI_LOGITS) {
@@ -754,9 +758,10 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
     }
     lds = std::max(lds, fattn_lds_bytes());
     grid += a.fattn_wgs;
-    // The appended consumers spin on the projection workgroups' granules: every workgroup of
-    // the grid must be resident at once (the consumers, dispatched last, could otherwise hold
-    // CUs a producer waits for).  One workgroup per CU always fits, so grid <= CUs suffices.
+    // The attention workgroups spin on the projection workgroups' granules (and those, with
+    // o_proj fused, on the attention's): every workgroup of the grid must be resident at once,
+    // whatever the dispatch order (fattn_first).  A 16-wave workgroup at 128 VGPRs fills a
+    // CU's register file, so each takes a CU of its own and grid <= CUs suffices.
     static const int cus = [] {
       int n = 0;
       int dev = 0;

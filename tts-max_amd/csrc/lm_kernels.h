@@ -117,6 +117,7 @@ struct WgemmArgs {
   AttnArgs fa;                // the attention of this layer (its output row: fa.out)
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
+  int fattn_first = 0;        // 1: the attention workgroups are the grid's first blocks
   int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
   // o_proj fused behind the attention (fo_units > 0): the attention workgroups also publish
   // the bf16 attention row as granules (gran + N/2, same tag); projection workgroup b <
