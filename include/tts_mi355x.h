@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TTS_ABI_VERSION 3
+#define TTS_ABI_VERSION 4
 
 typedef int32_t tts_status;
 enum {
@@ -175,6 +175,16 @@ tts_status tts_slots_release(tts_engine* e, int32_t slot);
 tts_status tts_lm_score(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
                         int32_t n_last, float* logits, void* stream);
 
+/* Teacher-forced scoring through the decode step: prefills the first lens[b] - n_last tokens
+ * of each sequence, then feeds the last n_last tokens one decode step at a time (all
+ * sequences as one batch: the kernels generate runs after its prefill) and writes each
+ * step's bf16-rounded logits as fp32.  Same positions as tts_lm_score.  gather_idx
+ * (optional, host [batch][n_last][k]) keeps only those vocabulary entries; with NULL,
+ * k is ignored and the full [batch][n_last][vocab] is written.  Needs lens[b] > n_last. */
+tts_status tts_lm_score_decode(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
+                               int32_t n_last, const int32_t* gather_idx, int32_t k, float* logits,
+                               void* stream);
+
 /* Maps token ids to speech codes through the loaded LUT (-1 for non-speech ids). */
 tts_status tts_lm_id_to_code(tts_engine* e, const int32_t* ids, int32_t n, int32_t* codes);
 
@@ -188,7 +198,8 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
  * accounting.  which: 0 qkv projection (+RMSNorm), 1 o_proj (+residual), 2 gate/up
  * (+RMSNorm, SwiGLU), 3 down_proj (+residual), 4 lm_head (+RMSNorm, penalty, argmax
  * partials), 5 decode attention (ctx = `ctx` positions), 6 qkv with the decode attention
- * fused in (one row).  rows = batch rows.
+ * fused in (one row), 7 the same launch also carrying o_proj (+residual; the one-row
+ * step's default form).  rows = batch rows.
  * Outputs: average ms per launch and the algorithmic HBM bytes one launch must move. */
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes);

@@ -200,6 +200,76 @@ def chain_fixture(name: str, manifest: dict) -> None:
                           "model (synth.apply_chain)", cases=stats, seconds=round(time.time() - t0, 1))
 
 
+# Teacher-forced logits through transformers' own DECODE path (prefill of a prefix, then one
+# cached forward per token with DynamicCache: what GenerationMixin._sample runs,
+# generation/utils.py:2783-2950) at the contexts the configs and the reference's defaults
+# reach: TTS-1 up to max_tokens = 1,792 total positions (inferencing.py:21,
+# tools/serving/inference.py:142), crossing the decode attention's 1,024-position pass at
+# head dim 64; TTS-1-Max's dims (2 layers) at configs[3]'s ~700 positions, crossing the
+# 512-position pass at head dim 128.  Sequences = a synthetic prompt + random speech ids
+# (teacher forcing needs no greedy continuation).  Stored per decode step: HF's top-16 ids
+# and 16 fixed random ids with their logits.
+# (arch, seed, [(utt, total length)], n_last)
+LONG_CASES = {
+    "lm_tts1_long": ("tts1", 0x5EED, [(0, 1792), (1, 1664), (2, 1536), (3, 1408)], 1200),
+    "lm_max2l_long": ("tts1-max-2l", 77, [(r, 760 - 20 * r) for r in range(8)], 560),
+}
+
+
+def hf_decode_logits(model, seq, n_last):
+    """transformers' cached decode over the last n_last tokens of seq (fp32 copies of the
+    bf16 logits, as _sample's `.float()`): [n_last, V]."""
+    p0 = len(seq) - n_last
+    out = []
+    with torch.no_grad():
+        r = model(torch.tensor([seq[:p0]]), use_cache=True, logits_to_keep=1)
+        pkv = r.past_key_values
+        for t in range(p0, len(seq)):
+            r = model(torch.tensor([[seq[t]]]), past_key_values=pkv, use_cache=True)
+            pkv = r.past_key_values
+            out.append(r.logits[0, -1].float())
+    return torch.stack(out)
+
+
+def long_fixture(name: str, manifest: dict) -> None:
+    arch_name, seed, seqs, n_last = LONG_CASES[name]
+    arch = configs.LM_ARCHS[arch_name]
+    vocab = configs.vocab_for(arch)
+    t0 = time.time()
+    w = synth.lm_weights_cpu(arch, seed)
+    model = hf_model(arch, w)
+    orc = lm_oracle.LlamaOracle(arch, w, max_seq_len=2048)
+    rec = dict(ids=[], lens=[], tf_idx=[], tf_val=[])
+    stats = []
+    for utt, L in seqs:
+        prompt = synth.synthetic_prompt(vocab, utt, 40, 150)
+        rng = np.random.default_rng(4321 + utt)
+        seq = prompt + [vocab.code_to_id(int(c)) for c in rng.integers(0, vocab.codebook_size, L - len(prompt))]
+        tf = hf_decode_logits(model, seq, n_last)
+        gen = torch.Generator().manual_seed(1000 + utt)
+        idx = torch.cat([torch.topk(tf, 16, dim=-1).indices,
+                         torch.randint(0, arch.vocab_size, (n_last, 16), generator=gen)], dim=1)
+        val = torch.gather(tf, 1, idx)
+        st = dict(utt=utt, L=L, n_last=n_last, first_pos=L - n_last, logit_absmax=float(tf.abs().max()))
+        if utt == seqs[0][0]:  # the CPU oracle (prefill form) on the first sequence
+            o = orc.score(seq, n_last)
+            dev = (torch.gather(o, 1, idx) - val).abs()
+            st.update(oracle_prefill_vs_hf_decode_max=float(dev.max()), oracle_prefill_vs_hf_decode_mean=float(dev.mean()))
+        stats.append(st)
+        rec["ids"] += seq
+        rec["lens"].append(L)
+        rec["tf_idx"].append(idx.numpy().astype(np.int32))
+        rec["tf_val"].append(val.numpy().astype(np.float32))
+        print(name, json.dumps(st), round(time.time() - t0), flush=True)
+    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), arch=arch_name, seed=seed, n_last=n_last,
+                        ids=np.asarray(rec["ids"], np.int32), lens=np.asarray(rec["lens"], np.int32),
+                        tf_idx=np.stack(rec["tf_idx"]), tf_val=np.stack(rec["tf_val"]))
+    manifest[name] = dict(kind="lm_decode_tf", arch=arch_name, seed=seed,
+                          generator="transformers.LlamaForCausalLM cached decode (DynamicCache, one token per "
+                          f"forward; transformers {__import__('transformers').__version__}, bf16, CPU, sdpa)",
+                          cases=stats, seconds=round(time.time() - t0, 1))
+
+
 # The synthesis composition (inferencing.py:110-159) executed by the reference's own
 # `_synthesize_audio`: transformers' generate on the tiny LM, the reference codec loaded by
 # its own `decoding.create` from a {"model": ...} checkpoint, a duck-typed tokenizer that
@@ -507,10 +577,11 @@ def main():
     mpath = os.path.join(GOLDEN, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     torch.manual_seed(0)
-    names = args.only or (list(LM_CASES) + list(CHAIN_CASES) + list(SYNTH_CASES) + list(CONFIG1_CASES) +
-                          list(CODEC_CASES) + list(ENCODER_CASES))
+    names = args.only or (list(LM_CASES) + list(CHAIN_CASES) + list(LONG_CASES) + list(SYNTH_CASES) +
+                          list(CONFIG1_CASES) + list(CODEC_CASES) + list(ENCODER_CASES))
     for n in names:
         fn = (lm_fixture if n in LM_CASES else chain_fixture if n in CHAIN_CASES else
+              long_fixture if n in LONG_CASES else
               synth_fixture if n in SYNTH_CASES else config1_fixture if n in CONFIG1_CASES else
               encoder_fixture if n in ENCODER_CASES else codec_fixture)
         fn(n, manifest)

@@ -31,7 +31,7 @@ def test_abi_version_and_error_path():
     from tts_amd import _lib
 
     lib = _lib.load_library()
-    assert lib.tts_abi_version() == 3
+    assert lib.tts_abi_version() == 4
     # invalid argument path: no GPU work, error message set, status non-zero
     st = lib.tts_engine_create(0, None)
     assert st != 0

@@ -1,0 +1,97 @@
+"""The one-row decode step's fused QKV + attention + o_proj launch (lm_gemm_kernel.h) under
+adverse conditions:
+
+* its grid order (projection workgroups, then attention, then o_proj workgroups) lets every
+  workgroup wait only on blocks of lower index, so it completes while other kernels hold CUs:
+  a B = 1 generation running beside prompt-audio encodes on a second engine and stream gives
+  the ids it gives alone;
+* a granule wait that gives up (forced with TTS_FATTN_SPINS=1) is reported at the first read
+  as an error, never returned as ids, and the engine stays usable."""
+
+import os
+import subprocess
+import sys
+import threading
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _tts1_prompt():
+    from tts_amd import configs, synth
+
+    return synth.synthetic_prompt(configs.vocab_for(configs.TTS1), 5, 39, 150)
+
+
+def test_b1_generation_beside_concurrent_encodes():
+    import torch
+
+    from tts_amd import configs, synth
+    from tts_amd.encoder import MI355XAudioEncoder
+    from tts_amd.speechlm import MI355XSpeechLM
+
+    arch = configs.TTS1
+    p = _tts1_prompt()
+    m = MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=1, max_seq_len=len(p) + 320)
+    kw = dict(max_length=len(p) + 300, min_new_tokens=300, eos_token_id=-1, repetition_penalty=1.1)
+    alone = m.generate_batch([p], **kw)[0]
+    enc = MI355XAudioEncoder.synthetic(device=0)
+    wav = torch.from_numpy(synth.synthetic_wav(3, 48000))[None]
+    feats = enc.features(wav)
+    ref_codes = enc.encode_from_features(wav[0].numpy(), feats)
+    stop, n_enc, errs = threading.Event(), [0], []
+
+    def encoder_loop():
+        try:
+            while not stop.is_set():
+                c = enc.encode_from_features(wav[0].numpy(), feats)
+                assert (c == ref_codes).all()
+                n_enc[0] += 1
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    t = threading.Thread(target=encoder_loop)
+    t.start()
+    try:
+        together = [m.generate_batch([p], **kw)[0] for _ in range(3)]
+    finally:
+        stop.set()
+        t.join()
+    assert not errs, errs
+    assert n_enc[0] >= 1
+    assert all(x == alone for x in together)
+    enc.close()
+    m.close()
+
+
+_SPIN_CHILD = r'''
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
+from tts_amd import configs, synth
+from tts_amd._lib import TtsError
+from tts_amd.speechlm import MI355XSpeechLM
+p = synth.synthetic_prompt(configs.vocab_for(configs.TTS1), 5, 39, 150)
+m = MI355XSpeechLM.synthetic(configs.TTS1, seed=0x5EED, max_batch=2, max_seq_len=len(p) + 80)
+kw = dict(max_length=len(p) + 64, min_new_tokens=64, eos_token_id=-1, repetition_penalty=1.1)
+for trial in range(2):  # the error is raised at the first read, and again on the next request
+    try:
+        m.generate_batch([p], **kw)
+        print("NO-ERROR")
+        sys.exit(0)
+    except TtsError as e:
+        assert "granule wait timed out" in str(e), e
+# the batched step (no fused launch) on the same engine still works
+two = m.generate_batch([p, p], **kw)
+assert two[0] == two[1] and len(two[0]) == 64
+print("RAISED")
+'''
+
+
+def test_fused_wait_timeout_raises_at_first_read():
+    r = subprocess.run([sys.executable, "-c", _SPIN_CHILD, ROOT], env=dict(os.environ, TTS_FATTN_SPINS="1"),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "RAISED", r.stdout

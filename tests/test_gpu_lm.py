@@ -368,3 +368,69 @@ def test_tts1_teacher_forced_logits_vs_transformers():
         json.dump(rec, f)
     assert d.max().item() <= TF_MAX, d.max().item()
     assert d.mean().item() <= TF_MEAN, d.mean().item()
+
+
+# engine-vs-transformers bars of the long-context decode comparisons (tests/golden/
+# lm_tts1_long.npz, lm_max2l_long.npz): the short-context bars above (TF_MAX / TF_MEAN for
+# TTS-1, 0.5 / 0.05 for the TTS-1-Max dims); the measured deviations are written to
+# gpurun_out/long_tf_dev_<fixture>.json and committed under profiles/
+LONG_BARS = {"lm_tts1_long": (TF_MAX, TF_MEAN), "lm_max2l_long": (0.5, 0.05)}
+
+
+def _long_case(name):
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    lens = z["lens"].tolist()
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    seqs = [z["ids"][offs[i]:offs[i + 1]].tolist() for i in range(len(lens))]
+    return str(z["arch"]), int(z["seed"]), int(z["n_last"]), seqs, z["tf_idx"], torch.from_numpy(z["tf_val"])
+
+
+@pytest.mark.parametrize("name,row_sets", [
+    ("lm_tts1_long", [[0], [0, 1, 2, 3], [0, 1, 2, 3] * 6]),   # fused one-row step; <=16 rows; 17..32 rows
+    ("lm_max2l_long", [[0], list(range(8))]),                  # head dim 128, configs[3]'s 8 rows per GPU
+])
+def test_decode_attention_long_context_vs_transformers(name, row_sets):
+    """The DECODE step's arithmetic (MI355XSpeechLM.score_decode: prefill of a prefix, then one
+    decode step per position) against transformers' own cached decode (oracle/make_golden.py
+    hf_decode_logits) at the contexts the reference's defaults reach: TTS-1 over positions
+    208..1,791 (max_tokens = 1,792, inferencing.py:21), crossing the decode attention's
+    1,024-position pass (16 waves x 64 positions at head dim 64, lm_attn_core.h); the TTS-1-Max
+    dims over positions 60..759 (configs[3]: P 202 + N 500), crossing the 512-position pass at
+    head dim 128.  Each row set runs as one batch: one row (TTS-1: the fused QKV + attention
+    + o_proj launch), <= 16 rows, 17..32 rows (the two-m-tile GEMVs).  Bars: the engine-vs-
+    transformers bars of the short-context tests; copies of a sequence must agree bit for
+    bit, and the argmax must be HF's wherever HF's top-2 margin exceeds 2 x the max bar."""
+    import json
+
+    from tts_amd import configs
+    from tts_amd.speechlm import MI355XSpeechLM
+
+    arch_name, seed, n_last, seqs, idx, val = _long_case(name)
+    bar_max, bar_mean = LONG_BARS[name]
+    arch = configs.LM_ARCHS[arch_name]
+    rows_max = max(len(r) for r in row_sets)
+    m = MI355XSpeechLM.synthetic(arch, seed=seed, max_batch=rows_max, max_seq_len=max(len(s) for s in seqs) + 8)
+    rec = {}
+    try:
+        for rs in row_sets:
+            got = m.score_decode([seqs[i] for i in rs], n_last, idx[rs])
+            ref = val[rs]
+            d = (got - ref).abs()
+            rec[len(rs)] = {"max_abs": d.max().item(), "mean_abs": d.mean().item(), "n": int(d.numel()),
+                            "first_pos": [len(seqs[i]) - n_last for i in sorted(set(rs))],
+                            "last_pos": [len(seqs[i]) - 1 for i in sorted(set(rs))]}
+            print(name, len(rs), "rows:", rec[len(rs)])
+            for j, i in enumerate(rs):  # copies of one sequence: identical bits
+                first = rs.index(i)
+                assert torch.equal(got[j], got[first]), (name, len(rs), j)
+            top2 = torch.topk(ref[:, :, :16], 2, dim=-1).values  # (HF's top-16 first: its own top-2)
+            decisive = (top2[..., 0] - top2[..., 1]) > 2 * bar_max
+            hit = got[:, :, :16].argmax(-1) == 0
+            assert bool(hit[decisive].all()), (name, len(rs), int((~hit & decisive).sum()))
+            assert d.max().item() <= bar_max, (name, len(rs), rec[len(rs)])
+            assert d.mean().item() <= bar_mean, (name, len(rs), rec[len(rs)])
+    finally:
+        m.close()
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", f"long_tf_dev_{name}.json"), "w") as f:
+            json.dump({"bars": [bar_max, bar_mean], "by_rows": rec}, f, indent=1)

@@ -53,7 +53,7 @@ def _run(rows, copies, new_n, **env):
 
 
 def test_tts1_max_full_depth_batch_properties():
-    rows, copies, new_n = 8, 2, 48
+    rows, copies, new_n = 8, 2, 500  # configs[3]: 500 codes (context to 702: the 512-position hd128 pass)
     a, b = _run(rows, copies, new_n)
     assert a == b  # graph replay: same ids
     assert all(len(x) == new_n for x in a)

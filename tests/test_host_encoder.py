@@ -47,3 +47,42 @@ def test_synthetic_weight_names_cover_the_fixture_model():
     assert len(names) == len(set(names)) == 195
     f = synth.kaiser_sinc_filter(0.25, 0.3, 12)
     assert abs(float(f.sum()) - 1.0) < 1e-6 and np.allclose(f.numpy(), f.numpy()[::-1])
+
+
+def test_caching_encoder_constructor_forms(monkeypatch, tmp_path):
+    """CachingAudioEncoder(model_path, device) as the reference builds it (encoding.py:59-63,
+    tools/serving/inference.py:115-116) goes through create(); an encoder object is wrapped
+    as is.  Both cache per prompt id."""
+    calls = []
+
+    class Fake:
+        def encode(self, wav):
+            calls.append("encode")
+            return torch.tensor([[3, 1, 4]]).reshape(-1)
+
+    def fake_create(model_path, device=0, w2v_path=None):
+        calls.append((model_path, device, w2v_path))
+        return Fake()
+
+    monkeypatch.setattr(encoder, "create", fake_create)
+    ck = tmp_path / "encoder.ckpt"
+    c1 = encoder.CachingAudioEncoder(str(ck), torch.device("cuda", 0))
+    assert calls == [(str(ck), torch.device("cuda", 0), None)]
+    c2 = encoder.CachingAudioEncoder(ck, "cuda:0", w2v_path="/local/w2v-bert-2.0")
+    assert calls[-1] == (str(ck), "cuda:0", "/local/w2v-bert-2.0")
+    c3 = encoder.CachingAudioEncoder(Fake())
+    for c in (c1, c2, c3):
+        n = calls.count("encode")
+        assert c.encode("p0", torch.zeros(1, 320)) == [3, 1, 4]
+        assert c.encode("p0", torch.zeros(1, 320)) == [3, 1, 4]
+        assert calls.count("encode") == n + 1
+
+
+def test_feature_extractor_front_end_check():
+    from transformers import SeamlessM4TFeatureExtractor
+
+    encoder.check_feature_extractor(SeamlessM4TFeatureExtractor(padding_value=1.0))
+    import pytest
+
+    with pytest.raises(ValueError):
+        encoder.check_feature_extractor(SeamlessM4TFeatureExtractor())  # padding_value 0.0

@@ -158,3 +158,31 @@ def test_encoder_oracle_reproduces_reference():
         assert np.abs(pre.numpy() - z["pre_round"][to:to + T]).max() < 5e-3
         wo += n
         to += T
+
+
+@pytest.mark.parametrize("name", ["lm_tts1_long", "lm_max2l_long"])
+def test_long_context_fixtures_well_formed(name):
+    """The decode-path teacher-forcing fixtures (transformers' cached decode, make_golden.py
+    LONG_CASES): every sequence decodes its last n_last positions, crossing the decode
+    attention's first pass (1,024 positions at head dim 64, 512 at head dim 128); the stored
+    HF top-16 values are sorted and finite; the prompt is the reference prompt shape.  (The CPU
+    oracle's agreement on these sequences is in the manifest: a 1,792-position forward is too
+    slow for this suite.)"""
+    import json
+
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    from tts_amd import configs
+
+    arch = configs.LM_ARCHS[str(z["arch"])]
+    lens, n_last = z["lens"], int(z["n_last"])
+    assert z["ids"].size == lens.sum() and z["tf_idx"].shape == (lens.size, n_last, 32)
+    assert z["tf_val"].shape == z["tf_idx"].shape and np.isfinite(z["tf_val"]).all()
+    top = z["tf_val"][:, :, :16]
+    assert (np.diff(top, axis=-1) <= 0).all()
+    assert ((z["tf_idx"] >= 0) & (z["tf_idx"] < arch.vocab_size)).all()
+    pass_len = 1024 if arch.head_dim == 64 else 512
+    assert int(lens.max()) > pass_len and int(lens.min()) - n_last < pass_len
+    vocab = configs.vocab_for(arch)
+    assert z["ids"][0] == vocab.bos_id
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))[name]
+    assert man["cases"][0]["oracle_prefill_vs_hf_decode_max"] <= 0.5

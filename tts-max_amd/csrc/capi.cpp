@@ -198,6 +198,17 @@ tts_status tts_lm_score(tts_engine* e, const int32_t* ids, const int32_t* lens, 
   });
 }
 
+tts_status tts_lm_score_decode(tts_engine* e, const int32_t* ids, const int32_t* lens, int32_t batch,
+                               int32_t n_last, const int32_t* gather_idx, int32_t k, float* logits,
+                               void* stream) {
+  return guarded([&] {
+    TTS_REQUIRE(e && ids && lens && logits && n_last >= 1, "bad argument");
+    Engine* E = reinterpret_cast<Engine*>(e);
+    HIP_CHECK(hipSetDevice(E->device));
+    lm_score_decode(E, ids, lens, batch, n_last, gather_idx, k, logits, pick_stream(E, stream));
+  });
+}
+
 tts_status tts_lm_id_to_code(tts_engine* e, const int32_t* ids, int32_t n, int32_t* codes) {
   return guarded([&] {
     TTS_REQUIRE(e && ids && codes && n >= 0, "bad argument");

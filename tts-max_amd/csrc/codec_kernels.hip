@@ -531,8 +531,9 @@ void launch_rmsnorm_f32(const float* x, int T, int C, const float* w, float eps,
   hipLaunchKernelGGL(rmsnorm_f32_kernel, dim3(T), dim3(256), 0, s, x, C, w, eps, y);
 }
 
-__global__ void layernorm_f32_kernel(const float* __restrict__ x, int C, const float* __restrict__ w,
-                                     const float* __restrict__ b, float eps, float* __restrict__ y) {
+// (x and y may alias: callers normalise in place; each thread rewrites only elements it read)
+__global__ void layernorm_f32_kernel(const float* x, int C, const float* __restrict__ w,
+                                     const float* __restrict__ b, float eps, float* y) {
   __shared__ float red[16];
   const float* xr = x + (size_t)blockIdx.x * C;
   float s1 = 0.f;

@@ -159,6 +159,8 @@ void lm_slots_read(Engine* e, int slot, int32_t* out_ids, int cap, int32_t* n_ou
 void lm_slots_release(Engine* e, int slot);
 void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
               float* logits, hipStream_t s);
+void lm_score_decode(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
+                     const int32_t* gidx, int k, float* out, hipStream_t s);
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes);
 

@@ -418,8 +418,13 @@ struct Ctx {
     fx.fattn_wgs = a.rows * a.KVH;
     fx.fattn_layer = layer;
     fx.fattn_err = w.ferr.as<int>();
-    static const bool first = !(getenv("TTS_FATTN_FIRST") && !atoi(getenv("TTS_FATTN_FIRST")));
+    // TTS_FATTN_FIRST=1: round 3's order (attention workgroups first, o_proj on the projection
+    // workgroups; needs the whole grid resident); default: the deadlock-free order
+    static const bool first = getenv("TTS_FATTN_FIRST") && atoi(getenv("TTS_FATTN_FIRST"));
     fx.fattn_first = first ? 1 : 0;
+    // TTS_FATTN_SPINS: polls before a granule wait gives up (tests drive the failure path with it)
+    static const int spins = getenv("TTS_FATTN_SPINS") ? std::max(1, atoi(getenv("TTS_FATTN_SPINS"))) : (1 << 16);
+    fx.fattn_spins = spins;
     if (with_oproj) {
       const LmLayer& ly = M.layers[layer];
       const WgemmPlan po = plan_wgemm(1, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu);
@@ -997,6 +1002,9 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   // (experiment hook TTS_BENCH_ONE_LAYER=1: every launch on layer 0, weights L2-warm when
   // they fit the XCDs' L2s — what a cross-kernel weight prefetch could at best buy)
   static const bool one_layer = getenv("TTS_BENCH_ONE_LAYER") && atoi(getenv("TTS_BENCH_ONE_LAYER"));
+  // (the fused launches tag their granules with (pos, layer): on one layer every launch would
+  // match the previous launch's granules and never wait — an optimistic, stale measurement)
+  TTS_REQUIRE(!(one_layer && which >= 6), "TTS_BENCH_ONE_LAYER cannot time the fused launches (selectors 6, 7)");
   int it_layer = 0;
   auto launch = [&]() {
     const int li = one_layer ? 0 : it_layer++ % c.num_layers;
@@ -1087,6 +1095,81 @@ void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_l
     uint32_t u = (uint32_t)h[i] << 16;
     memcpy(&logits[i], &u, 4);
   }
+}
+
+// Teacher forcing through the DECODE step's kernels (the path generate runs after prefill):
+// prefill the first lens[b] - n_last tokens of every sequence, then feed the remaining
+// n_last tokens one decode step at a time (all rows together, the step's launch sequence:
+// fused QKV+attention(+o_proj) at one row, the batched GEMVs and the (row, kv head) decode
+// attention otherwise) and keep each step's bf16 logits.  Same positions as lm_score, so
+// the two differ only by prefill vs decode arithmetic.  gidx (optional, [B][n_last][k]):
+// keep only those vocabulary entries; otherwise k = V.
+void lm_score_decode(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_last,
+                     const int32_t* gidx, int k, float* out, hipStream_t s) {
+  TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
+  TTS_REQUIRE(B >= 1 && B <= e->w.cap_batch, "batch out of range");
+  Ctx X(e, s);
+  const tts_lm_config& c = X.c;
+  const int V = c.vocab_size, HID = c.hidden_size;
+  if (!gidx) k = V;
+  TTS_REQUIRE(k >= 1 && k <= V, "bad gather width");
+  std::vector<int> start(B), plen(B);
+  for (int b = 0, off = 0; b < B; off += lens[b], ++b) {
+    TTS_REQUIRE(lens[b] > n_last && lens[b] <= c.max_seq_len, "bad sequence length (needs lens > n_last)");
+    start[b] = off;
+    plen[b] = lens[b] - n_last;
+  }
+  if (gidx)
+    for (size_t i = 0; i < (size_t)B * n_last * k; ++i) TTS_REQUIRE(gidx[i] >= 0 && gidx[i] < V, "gather index out of range");
+  // ---- prefill the prefixes (groups of whole prefixes that fit the workspace)
+  {
+    std::vector<int> last_rows;
+    int b0 = 0;
+    while (b0 < B) {
+      int b1 = b0, grp = 0;
+      std::vector<int32_t> pid;
+      while (b1 < B && grp + plen[b1] <= e->w.cap_rows) {
+        pid.insert(pid.end(), ids + start[b1], ids + start[b1] + plen[b1]);
+        grp += plen[b1++];
+      }
+      TTS_REQUIRE(b1 > b0, "a prefix is longer than the prefill workspace");
+      int rows = 0;
+      prefill_rows_setup(X, pid.data(), plen.data() + b0, b1 - b0, b0, last_rows, rows);
+      X.layers(rows, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), false);
+      b0 = b1;
+    }
+  }
+  // ---- n_last decode steps with the given tokens
+  std::vector<int> ident(B), tok(B), pos(B);
+  for (int b = 0; b < B; ++b) ident[b] = b;
+  DevBuf lg;
+  lg.alloc((size_t)B * V * 2);
+  std::vector<uint16_t> h((size_t)B * V);
+  HIP_CHECK(hipMemcpyAsync(e->w.row_slot.p, ident.data(), B * 4, hipMemcpyHostToDevice, s));
+  for (int i = 0; i < n_last; ++i) {
+    for (int b = 0; b < B; ++b) {
+      tok[b] = ids[start[b] + plen[b] + i];
+      pos[b] = plen[b] + i;
+    }
+    HIP_CHECK(hipMemcpyAsync(e->w.row_idx.p, tok.data(), B * 4, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(e->w.row_pos.p, pos.data(), B * 4, hipMemcpyHostToDevice, s));
+    launch_embed(e->w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), B, HID, s);
+    X.layers(B, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
+    X.gemm(e->w.x.as<bf16_t>(), B, HID, X.M.lm_head, V, X.M.final_norm, lg.as<bf16_t>(), V, nullptr, EPI_STORE);
+    check_launch();
+    HIP_CHECK(hipMemcpyAsync(h.data(), lg.p, h.size() * 2, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));  // (h and the token/position vectors are reused)
+    for (int b = 0; b < B; ++b) {
+      float* o = out + ((size_t)b * n_last + i) * k;
+      const uint16_t* hb = h.data() + (size_t)b * V;
+      const int32_t* gi = gidx ? gidx + ((size_t)b * n_last + i) * k : nullptr;
+      for (int j = 0; j < k; ++j) {
+        const uint32_t u = (uint32_t)hb[gi ? gi[j] : j] << 16;
+        memcpy(&o[j], &u, 4);
+      }
+    }
+  }
+  check_fattn(e, s);
 }
 
 }  // namespace tts

@@ -38,7 +38,22 @@ constexpr size_t fattn_lds_bytes() {
   return (size_t)DEC_G * FATTN_D * 4 + (DEC_G * FATTN_D / 2 + FATTN_D) * 4 + 2 * FATTN_D * 2 +
          (size_t)dec_red_floats<FATTN_D, DEC_NW>() * 4;
 }
-constexpr int FATTN_MAX_SPINS = 1 << 16;  // ~0.1 s: the wait always ends (fattn_err set)
+// A bounded granule wait: polls until `ready()` or `spins` polls; on timeout it sets the error
+// flag, and every later wait (this launch or the following ones) that finds the flag set
+// (checked every 512 polls, so never on a wait that succeeds quickly) gives up at once — a
+// failure costs one timeout, then the results are garbage and the host raises at the next read
+template <typename Poll>
+TTS_DEV bool fattn_wait(Poll ready, int* err, int spins, bool report) {
+  for (int n = 1; !ready(); ++n) {
+    if (n > spins) {
+      if (report) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if ((n & 511) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
 
 template <int NT>
 TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
@@ -78,16 +93,11 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
     else if (tid < nq + D / 2) col = a.H * D + kvh * D + 2 * (tid - nq);
     else col = a.H * D + a.KVH * D + kvh * D + 2 * (tid - nq - D / 2);
     const uint64_t* gp = wa.gran + (size_t)row * (a.ld_qkv / 2) + col / 2;
-    uint64_t v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while ((uint32_t)(v >> 32) != tag) {
-      if (++spins > FATTN_MAX_SPINS) {
-        __hip_atomic_store(wa.fattn_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+    uint64_t v;
+    fattn_wait([&] {
       v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+      return (uint32_t)(v >> 32) == tag;
+    }, wa.fattn_err, wa.fattn_spins, true);
     raw[tid] = (uint32_t)v;
   }
   lds_barrier();
@@ -136,16 +146,11 @@ TTS_DEV void fused_oproj(const WgemmArgs& a, bf16_t* xs, float* red, int wave, i
                                               ((((long long)st * nr + u) * KSPLIT + kpart) * KU + kk) * 64 + lane);
   const bf16_t rr = a.fo_resid[u * 16 + (lane & 15)];
   const uint64_t* g = a.gran + a.N / 2 + kpart * 64 + lane;
-  uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int spins = 0;
-  while (!__all((uint32_t)(v >> 32) == tag)) {
-    if (++spins > FATTN_MAX_SPINS) {
-      if (lane == 0) __hip_atomic_store(a.fattn_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
+  uint64_t v;
+  fattn_wait([&] {
     v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+    return (bool)__all((uint32_t)(v >> 32) == tag);
+  }, a.fattn_err, a.fattn_spins, lane == 0);
   // this wave's 128 attention values into its own K range of the LDS row (read back by this
   // wave only: LDS operations of one wave complete in order)
   *(uint32_t*)(xs + kpart * 128 + 2 * lane) = (uint32_t)v;
@@ -201,13 +206,25 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
   constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && NORM && EARLY && WAVES == DEC_NW;
+  // fused launch (a.fattn_wgs): the grid's projection / attention / o_proj workgroups
+  // (WgemmArgs::fattn_first for the two orders)
+  const int fo_wgs = (FATT && a.fattn_wgs && !a.fattn_first) ? a.fo_units : 0;  // o_proj workgroups (order 0)
+  const int nproj = (int)gridDim.x - (FATT ? a.fattn_wgs : 0) - fo_wgs;
   if constexpr (FATT) {
-    // the attention workgroups: the grid's first fattn_wgs blocks (fattn_first: dispatched
-    // first, their K / V loads ahead of the projection's weight stream) or its last ones
-    const int cb = a.fattn_first ? (int)blockIdx.x : (int)blockIdx.x - ((int)gridDim.x - a.fattn_wgs);
-    if (a.fattn_wgs && cb >= 0 && cb < a.fattn_wgs) {
-      fattn_consumer<NT>(a, smem, cb);
-      return;
+    if (a.fattn_wgs) {
+      const int cb = a.fattn_first ? (int)blockIdx.x : (int)blockIdx.x - nproj;
+      if (cb >= 0 && cb < a.fattn_wgs) {
+        fattn_consumer<NT>(a, smem, cb);
+        return;
+      }
+      if (cb >= a.fattn_wgs) {  // (order 0) o_proj unit cb - fattn_wgs
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const uint32_t tag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
+        const size_t xs_bytes = (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15);
+        fused_oproj<KU, KSPLIT, R>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane, tag, cb - a.fattn_wgs);
+        return;
+      }
     }
   }
   constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
@@ -240,7 +257,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   const int kt_base = a.sliced ? blockIdx.y * KTc : 0;      // first k-tile held in A
   const bf16_t* xg = a.x ? a.x + (a.sliced ? (size_t)blockIdx.y * a.K : 0) : nullptr;
   const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
-  const int ustride = (gridDim.x - a.fattn_wgs) * UPW;  // (appended attention workgroups excluded)
+  const int ustride = nproj * UPW;  // (the fused launch's attention / o_proj workgroups excluded)
 
   bf16_t* xs = (bf16_t*)smem;
   const size_t xs_bytes = (ASRC != A_GLOBAL) ? (((size_t)M * ldxs * 2 + 15) & ~(size_t)15) : 0;
@@ -683,7 +700,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   }
 
   if constexpr (FATT) {
-    if (a.fattn_wgs && a.fo_units > 0 && bx < a.fo_units) {
+    if (a.fattn_wgs && a.fattn_first && a.fo_units > 0 && bx < a.fo_units) {
       lds_barrier();  // (every wave past the QKV unit's LDS use)
       fused_oproj<KU, KSPLIT, R>(a, xs, red, wave, lane, ftag, bx);
     }
@@ -750,26 +767,28 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
           a.gran && a.fattn_err && !a.sliced))
       throw std::runtime_error("wgemm: fused attention needs the one-row 16-wave QKV launch (D 64)");
     if (!EARLY) throw std::runtime_error("wgemm: fused attention needs the register-staged prologue");
-    if (a.fo_units) {  // fused o_proj: one unit per projection workgroup, one granule per lane
+    if (a.fo_units) {  // fused o_proj: one unit per o_proj (order 1: projection) workgroup, one granule per lane
       const int S = (a.fa.H * a.fa.D / 32) / (KSPLIT * KU);
-      if (!(a.fo_w && a.fo_resid && a.fo_units <= grid && a.fo_units <= a.fo_ur && S == R &&
-            a.fa.H * a.fa.D == KSPLIT * 128 && KSPLIT == WAVES))
+      if (!(a.fo_w && a.fo_resid && (!a.fattn_first || a.fo_units <= grid) && a.fo_units <= a.fo_ur && S == R &&
+            a.fa.H * a.fa.D == KSPLIT * 128 && KSPLIT == WAVES && (size_t)a.M * (a.K + 8) * 2 >= (size_t)KSPLIT * 256))
         throw std::runtime_error("wgemm: fused o_proj shape mismatch");
     }
     lds = std::max(lds, fattn_lds_bytes());
-    grid += a.fattn_wgs;
-    // The attention workgroups spin on the projection workgroups' granules (and those, with
-    // o_proj fused, on the attention's): every workgroup of the grid must be resident at once,
-    // whatever the dispatch order (fattn_first).  A 16-wave workgroup at 128 VGPRs fills a
-    // CU's register file, so each takes a CU of its own and grid <= CUs suffices.
-    static const int cus = [] {
-      int n = 0;
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      return n;
-    }();
-    if (grid > cus) throw std::runtime_error("wgemm: fused attention grid exceeds one workgroup per CU");
+    grid += a.fattn_wgs + (a.fattn_first ? 0 : a.fo_units);
+    if (a.fattn_first) {
+      // order 1: the attention workgroups spin on the projection workgroups' granules and
+      // those (o_proj fused) on the attention's: every workgroup must be resident at once.
+      // A 16-wave workgroup at 128 VGPRs fills a CU's register file (one per CU), so
+      // grid <= CUs is required — and still not sufficient when other work shares the GPU
+      static const int cus = [] {
+        int n = 0;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
+      }();
+      if (grid > cus) throw std::runtime_error("wgemm: fused attention grid exceeds one workgroup per CU");
+    }
   }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
   const dim3 g(grid, a.sliced ? a.kc : 1);

@@ -117,13 +117,20 @@ struct WgemmArgs {
   AttnArgs fa;                // the attention of this layer (its output row: fa.out)
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
-  int fattn_first = 0;        // 1: the attention workgroups are the grid's first blocks
-  int* fattn_err = nullptr;   // set to 1 if a granule wait timed out
+  // grid order.  0 (default): the projection workgroups, then the attention workgroups, then
+  // (fo_units > 0) one o_proj workgroup per o_proj unit: every workgroup waits only on blocks
+  // of lower index, and blocks are dispatched in index order, so the launch completes whatever
+  // else occupies the GPU (no co-residency needed).  1 (round-3 order, TTS_FATTN_FIRST=1): the
+  // attention workgroups first and o_proj on the projection workgroups after their QKV unit —
+  // circular waits, so it needs the whole grid resident (grid <= CUs, checked at launch).
+  int fattn_first = 0;
+  int* fattn_err = nullptr;   // set to 1 if a granule wait timed out; later waits then give up at once
+  int fattn_spins = 1 << 16;  // polls (s_sleep 1 each, ~0.1 s in all) before a wait gives up
   // o_proj fused behind the attention (fo_units > 0): the attention workgroups also publish
-  // the bf16 attention row as granules (gran + N/2, same tag); projection workgroup b <
-  // fo_units then computes o_proj unit b (tiled weights fo_w, layout rounds fo_ur, one round)
-  // with the residual epilogue on fo_resid (the hidden row), its o_proj weights loaded while
-  // the attention runs
+  // the bf16 attention row as granules (gran + N/2, same tag); o_proj unit b (tiled weights
+  // fo_w, layout rounds fo_ur, one round) runs on the grid's b-th o_proj workgroup (order 0)
+  // or on projection workgroup b after its QKV unit (order 1), with the residual epilogue on
+  // fo_resid (the hidden row), its o_proj weights loaded while the attention runs
   const bf16_t* fo_w = nullptr;
   int fo_units = 0, fo_ur = 0;
   bf16_t* fo_resid = nullptr;

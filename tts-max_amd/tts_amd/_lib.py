@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "tts_slots_read",
     "tts_slots_release",
     "tts_lm_score",
+    "tts_lm_score_decode",
     "tts_lm_id_to_code",
     "tts_lm_last_timing",
     "tts_lm_bench_kernel",
@@ -168,6 +169,7 @@ def load_library() -> ctypes.CDLL:
         "tts_slots_read": (I32, [P, I32, pi32, I32, pi32, pi32]),
         "tts_slots_release": (I32, [P, I32]),
         "tts_lm_score": (I32, [P, pi32, pi32, I32, I32, ctypes.POINTER(ctypes.c_float), P]),
+        "tts_lm_score_decode": (I32, [P, pi32, pi32, I32, I32, pi32, I32, ctypes.POINTER(ctypes.c_float), P]),
         "tts_lm_id_to_code": (I32, [P, pi32, I32, pi32]),
         "tts_lm_last_timing": (I32, [P, ctypes.POINTER(F32), ctypes.POINTER(F32), pi32]),
         "tts_lm_bench_kernel": (I32, [P, I32, I32, I32, I32, ctypes.POINTER(F32), ctypes.POINTER(ctypes.c_double)]),

@@ -139,12 +139,14 @@ def run_sharded(prompts: Sequence[Sequence[int]] | None, n_items: int, work: Cal
 def synthesize_sharded(prompts: Sequence[Sequence[int]] | None, lm, decoder, device, *, max_new: int,
                        prompt_codes: Callable[[list[int]], list[int]], to_codes: Callable[[list[int]], list[int]],
                        balance: str = "contiguous", min_new_tokens: int = 0, eos_token_id: int = -1,
-                       repetition_penalty: float = 1.0, costs: Sequence[int] | None = None, wav_out=None):
+                       repetition_penalty: float = 1.0, costs: Sequence[int] | None = None, wav_out=None,
+                       wav_to_host: bool = True):
     """The whole DP job of BASELINE configs[3] / SURVEY §8e on this rank: broadcast the
     request batch from rank 0, generate this rank's shard (greedy, `max_length` = longest
     prompt + max_new), voice prompt codes + generated codes with the codec (one ragged
     batch), gather codes AND waveforms to rank 0.  Returns (ids, wavs) on rank 0 (lists in
-    request order), (None, None) elsewhere, plus this rank's (n_codes, n_items)."""
+    request order; the waveforms as host tensors unless wav_to_host=False), (None, None)
+    elsewhere, plus this rank's (n_codes, n_items)."""
     import torch.distributed as dist
 
     allp = broadcast_requests(prompts, device)
@@ -166,4 +168,6 @@ def synthesize_sharded(prompts: Sequence[Sequence[int]] | None, lm, decoder, dev
     n_codes = sum(len(v) for v in ids.values())
     if g_ids is None:
         return None, None, (n_codes, len(mine))
+    if wav_to_host:  # AudioDecoder.decode's boundary: waveforms in host memory (decoding.py:84-89)
+        g_wav = [w.cpu() for w in g_wav]
     return [t.tolist() for t in g_ids], g_wav, (n_codes, len(mine))

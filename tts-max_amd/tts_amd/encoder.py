@@ -20,6 +20,8 @@ from __future__ import annotations
 import abc
 import ctypes
 
+import os
+
 import numpy as np
 import torch
 
@@ -155,10 +157,19 @@ class MI355XAudioEncoder(AudioEncoderInterface):
 
 
 class CachingAudioEncoder:
-    """encoding.py:55-72: encodes a prompt once per prompt id; codes as a Python list."""
+    """encoding.py:55-72: encodes a prompt once per prompt id; codes as a Python list.
 
-    def __init__(self, encoder: AudioEncoderInterface):
-        self._encoder = encoder
+    Constructed as the reference does, ``CachingAudioEncoder(model_path, device)``
+    (encoding.py:59-63, called so at tools/serving/inference.py:115-116; the encoder comes from
+    ``create``, with ``w2v_path`` = a local facebook/w2v-bert-2.0 when the checkpoint lacks
+    it), or around an already built encoder object."""
+
+    def __init__(self, model_path: "str | os.PathLike | AudioEncoderInterface",
+                 device: "torch.device | str | int | None" = 0, *, w2v_path: str | None = None):
+        if isinstance(model_path, (str, os.PathLike)):
+            self._encoder = create(model_path=os.fspath(model_path), device=device, w2v_path=w2v_path)
+        else:
+            self._encoder = model_path
         self._prompt_encoding_cache: dict[str, list[int]] = {}
 
     @torch.no_grad()
@@ -191,6 +202,17 @@ def load_encoder_checkpoint(path: str) -> dict[str, torch.Tensor]:
     return dict(ckpt)
 
 
+# the w2v-bert-2.0 front end the encoder's weights expect (feature projection input =
+# num_mel_bins x stride = 160; 16 kHz; padding with 1.0 as the hub preprocessor_config)
+W2V_FEATURES = dict(feature_size=80, num_mel_bins=80, stride=2, sampling_rate=16000, padding_value=1.0)
+
+
+def check_feature_extractor(fe) -> None:
+    bad = {k: getattr(fe, k, None) for k, v in W2V_FEATURES.items() if getattr(fe, k, None) != v}
+    if bad:
+        raise ValueError(f"feature extractor differs from the w2v-bert-2.0 front end {W2V_FEATURES}: {bad}")
+
+
 def create(model_path: str, device: "torch.device | str | int | None" = 0,
            w2v_path: str | None = None) -> MI355XAudioEncoder:
     """encoding.create (75-80): the encoder from its checkpoint.  The reference loads
@@ -207,7 +229,14 @@ def create(model_path: str, device: "torch.device | str | int | None" = 0,
         m = transformers.Wav2Vec2BertModel.from_pretrained(w2v_path)
         for k, v in m.state_dict().items():
             w["wav2vec_model." + k] = v
-    fe = (transformers.SeamlessM4TFeatureExtractor.from_pretrained(w2v_path) if w2v_path
-          else transformers.SeamlessM4TFeatureExtractor(padding_value=1.0))
+    if w2v_path:
+        fe = transformers.SeamlessM4TFeatureExtractor.from_pretrained(w2v_path)
+    else:
+        # no preprocessor_config.json at hand: the w2v-bert-2.0 hub values (padding_value 1.0;
+        # the rest are SeamlessM4TFeatureExtractor's defaults).  Those hub values cannot be
+        # read offline, so the features of real weights are PARITY UNPINNED;
+        # the parameters the encoder depends on are checked here
+        fe = transformers.SeamlessM4TFeatureExtractor(padding_value=1.0)
+    check_feature_extractor(fe)
     dev = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
     return MI355XAudioEncoder(w, fe, device=dev.index or 0)

@@ -321,6 +321,31 @@ class MI355XSpeechLM:
                                           out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), None))
         return torch.from_numpy(out)
 
+    def score_decode(self, sequences: Sequence[Sequence[int]], n_last: int,
+                     gather_idx: np.ndarray | None = None) -> torch.Tensor:
+        """Teacher-forced bf16 logits (as fp32) of the last n_last positions computed by the
+        DECODE step (prefill of the prefixes, then one decode step per position, all sequences
+        as one batch): [B, n_last, V], or [B, n_last, k] at gather_idx [B, n_last, k]."""
+        with self.lock:
+            self._take_from_batcher()
+            B = len(sequences)
+            lens = np.array([len(s) for s in sequences], dtype=np.int32)
+            flat = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32) for s in sequences]))
+            pi32 = ctypes.POINTER(ctypes.c_int32)
+            if gather_idx is not None:
+                gi = np.ascontiguousarray(np.asarray(gather_idx, dtype=np.int32))
+                if gi.ndim != 3 or gi.shape[:2] != (B, n_last):
+                    raise ValueError("gather_idx must be [batch, n_last, k]")
+                k = gi.shape[2]
+                gptr = gi.ctypes.data_as(pi32)
+            else:
+                k, gptr = self.arch.vocab_size, None
+            out = np.zeros((B, n_last, k), dtype=np.float32)
+            _lib.check(self._lib.tts_lm_score_decode(self._h, flat.ctypes.data_as(pi32), lens.ctypes.data_as(pi32), B,
+                                                     n_last, gptr, k,
+                                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), None))
+            return torch.from_numpy(out)
+
     def last_timing(self) -> tuple[float, float, int]:
         a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int32()
         _lib.check(self._lib.tts_lm_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
