@@ -239,6 +239,14 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.gran.alloc((size_t)(QKV + H * D) / 2 * 8);  // q|k|v granules, then the attention row's
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
+  {  // batched decode attention: chunks of ~128 positions (4 waves x 32) over the longest
+     // context, 2..16 per (row, kv head); TTS_ATTN_SPLIT=<n> forces n (<= 1: one workgroup)
+    const char* ev = getenv("TTS_ATTN_SPLIT");
+    int ns = std::min(16, std::max(2, (S + 127) / 128));
+    if (ev) ns = std::min(16, atoi(ev));
+    w.attn_splits = ns;
+    if (ns > 1) w.apart.alloc((size_t)B * KVH * ns * (8 + 4 * D) * 4);
+  }
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
   {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
     const int kmax = std::max(HID, std::max(FF, H * D));
@@ -297,6 +305,13 @@ bool use_fused_oproj() {
   return v;
 }
 
+// 17..32 rows: RMSNorm in the GEMM's LDS prologue (rows landed by LDS-DMA, a wave per row)
+// instead of a standalone launch — experiment hook TTS_NORM32=1 (round 2 measured it slower)
+bool norm_in_lds32() {
+  static const bool v = getenv("TTS_NORM32") && atoi(getenv("TTS_NORM32"));
+  return v;
+}
+
 struct Ctx {
   Engine* e;
   hipStream_t s;
@@ -351,7 +366,7 @@ struct Ctx {
       if (norm && m > 16 && normw == ready && x == w.x.as<bf16_t>()) {
         xin = w.xn.as<bf16_t>() + (size_t)r0 * K;
         norm = false;
-      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || m > 16)) {
+      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || (m > 16 && !norm_in_lds32()))) {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
@@ -401,6 +416,10 @@ struct Ctx {
     a.q_rot = w.q_rot.as<bf16_t>(); a.out = w.attn_out.as<bf16_t>();
     a.blocks = w.blocks.as<int4>(); a.nblocks = w.nblocks;
     a.stamps = stamp_buf();
+    if (decode && rows > 1 && w.attn_splits > 1) {  // (one row: the fused launch's single-workgroup form)
+      a.splits = w.attn_splits;
+      a.part = w.apart.as<float>();
+    }
     return a;
   }
 

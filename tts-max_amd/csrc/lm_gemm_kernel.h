@@ -821,8 +821,9 @@ template <int C, int NG, int ASRC, bool NORM, int EPI>
 static void launch_shape(const WgemmArgs& a, int grid, hipStream_t s) {
   constexpr Shape3 h = kShapes[C];
   const int S = (a.K / 32) / (h.ksplit * h.ku);  // (sliced: stages of one chunk)
-  // (A_GLOBAL rides A fragments in the ring: one stage deep where two would spill)
-  const bool agr_r1 = ASRC == A_GLOBAL && (h.ku >= 4 || a.M > 16);
+  // (A_GLOBAL rides A fragments in the ring: one stage deep where two would spill — KU 4, or
+  // two m-tiles at KU > 2)
+  const bool agr_r1 = ASRC == A_GLOBAL && (h.ku >= 4 || (a.M > 16 && h.ku > 2));
   if (h.r >= 2 && S % 2 == 0 && !agr_r1) launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 2>(a, grid, s);
   else launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 1>(a, grid, s);
 }

@@ -58,6 +58,11 @@ struct AttnArgs {
   const int4* blocks = nullptr;  // prefill: query blocks {first row, rows (<= 16), slot, first position}
   int nblocks = 0;
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS)
+  // batched decode (rows > 1): the context of each (row, kv head) split into `splits` chunks
+  // over as many workgroups (flash-decoding partials in `part`, merged by a second kernel);
+  // splits <= 1: one workgroup per (row, kv head)
+  int splits = 0;
+  float* part = nullptr;  // [rows][KVH][splits][2*4 + 4*D] fp32
 };
 
 // ---- sampling / bookkeeping state of a decode step (lm_ops.hip, lm_finalize.h)
