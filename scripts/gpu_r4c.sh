@@ -12,6 +12,8 @@ timeout -k 10 600 python scripts/env_ab_probe.py TTS_AGR32 32 2 > $O/${T}_ab_agr
 AB_V0=1 AB_V1=6 timeout -k 10 600 python scripts/env_ab_probe.py TTS_ATTN_SPLIT 32 2 > $O/${T}_ab_split32.txt 2>&1 && \
 AB_V0=1 AB_V1=6 timeout -k 10 600 python scripts/env_ab_probe.py TTS_ATTN_SPLIT 8 2 > $O/${T}_ab_split8.txt 2>&1 && \
 timeout -k 10 600 python scripts/env_ab_probe.py TTS_NORM32 32 2 > $O/${T}_ab_norm32.txt 2>&1 && \
+timeout -k 10 600 python scripts/env_ab_probe.py TTS_CSPLIT32 32 2 > $O/${T}_ab_csplit32.txt 2>&1 && \
+timeout -k 10 600 python scripts/env_ab_probe.py TTS_COMBINE_FIXED 32 2 > $O/${T}_ab_combine32.txt 2>&1 && \
 timeout -k 10 300 python scripts/stamp_probe.py 450 32 > $O/${T}_stamps32.txt 2>&1 && \
 timeout -k 10 300 python scripts/codec_gemm_probe.py > $O/${T}_codec_gemm.txt 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof_max -o run -- \

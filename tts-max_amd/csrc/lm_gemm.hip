@@ -153,9 +153,10 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   // range; instead each wave loads its A fragments beside its weight tiles (A_GLOBAL ring, L2
   // hits).  TTS_AGR32=0: LDS staging (experiment hook)
   static const bool agr32 = !(getenv("TTS_AGR32") && !atoi(getenv("TTS_AGR32")));
+  bool agr_rows32 = false;
   if (agr32 && M > 16 && M <= 32 && p.sp.kc == 1 && (epi == EPI_STORE || epi == EPI_RESID) && p.sp.ku <= 2) {
     p.a_lds = false;
-    return p;
+    agr_rows32 = true;
   }
   if (!p.a_lds && p.sp.kc > 1 && (epi == EPI_STORE || epi == EPI_RESID) &&
       wgemm_lds_bytes(w, ks, ng, M, K / p.sp.kc, true) <= kLdsBudget) {
@@ -175,7 +176,11 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   static const int csplit_mode = getenv("TTS_CSPLIT") ? atoi(getenv("TTS_CSPLIT")) : 1;
   const int units = (N / 16) / ng;
   const int upw = w / ks;
-  if (csplit_mode > 0 && (M <= 16 || csplit_mode == 2) && !p.sliced && p.a_lds &&
+  // (17..32 rows with A from L2: the halves' waves load the same A fragments, L2 hits;
+  // TTS_CSPLIT32=0: off)
+  static const bool csplit32 = !(getenv("TTS_CSPLIT32") && !atoi(getenv("TTS_CSPLIT32")));
+  if (csplit_mode > 0 && (M <= 16 || csplit_mode == 2 || (agr_rows32 && csplit32)) && !p.sliced &&
+      (p.a_lds || agr_rows32) &&
       (epi == EPI_STORE || epi == EPI_RESID) && p.grid * upw >= units && 2 * units <= num_cu * upw) {
     p.csplit = 2;
     p.grid = (2 * units + upw - 1) / upw;

@@ -268,10 +268,75 @@ __global__ __launch_bounds__(256) void splitk_combine_norm_kernel(
   }
 }
 
+// The same arithmetic with every load in flight at once (the KC chunk partials, the residual
+// and the norm weight of the thread's IT chunks, issued before the first add): N = IT * 2048,
+// kc = KC.  TTS-1's down at 17..32 rows (4 chunks) and TTS-1-Max's (7 chunks, N 4096).
+template <int KC, int IT>
+__global__ __launch_bounds__(256) void splitk_combine_norm_fixed_kernel(
+    const float* __restrict__ part, int M, int ldp, bf16_t* __restrict__ resid, int ldo,
+    const bf16_t* __restrict__ normw, float eps, bf16_t* __restrict__ xn, int ldn) {
+  __shared__ float segs[64];
+  constexpr int N = IT * 2048;
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bf16_t* r = resid + (size_t)m * ldo;
+  float4 pa[IT][KC], pb[IT][KC];
+  u32x4_t old[IT], g[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = (wave * 64 + it * 256 + lane) * 8;  // (the generic kernel's chunk order)
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const float4* q = (const float4*)(part + ((size_t)k * M + m) * ldp + n);
+      pa[it][k] = q[0];
+      pb[it][k] = q[1];
+    }
+    old[it] = *(const u32x4_t*)(r + n);
+    g[it] = *(const u32x4_t*)(normw + n);
+  }
+  u32x4_t keep[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    float v[8] = {pa[it][0].x, pa[it][0].y, pa[it][0].z, pa[it][0].w, pb[it][0].x, pb[it][0].y, pb[it][0].z, pb[it][0].w};
+#pragma unroll
+    for (int k = 1; k < KC; ++k) {  // chunk order, as the generic kernel
+      v[0] += pa[it][k].x; v[1] += pa[it][k].y; v[2] += pa[it][k].z; v[3] += pa[it][k].w;
+      v[4] += pb[it][k].x; v[5] += pb[it][k].y; v[6] += pb[it][k].z; v[7] += pb[it][k].w;
+    }
+    u32x4_t pk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pk[q] = pack_bf2(bf_lo(old[it][q]) + rbf(v[2 * q]), bf_hi(old[it][q]) + rbf(v[2 * q + 1]));
+    *(u32x4_t*)(r + (wave * 64 + it * 256 + lane) * 8) = pk;
+    keep[it] = pk;
+    const float ssum = wave_sum_dpp(chunk_sumsq(pk));
+    if (lane == 0) segs[wave + 4 * it] = ssum;
+  }
+  __syncthreads();
+  float ss = 0.f;
+#pragma unroll
+  for (int sg = 0; sg < N / 512; ++sg) ss += segs[sg];
+  const float rs = 1.0f / sqrtf(ss / (float)N + eps);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    u32x4_t v = keep[it];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = pack_bf2(rbf(bf_lo(g[it][q]) * rbf(bf_lo(v[q]) * rs)), rbf(bf_hi(g[it][q]) * rbf(bf_hi(v[q]) * rs)));
+    *(u32x4_t*)(xn + (size_t)m * ldn + (wave * 64 + it * 256 + lane) * 8) = v;
+  }
+}
+
 void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp, bf16_t* resid, int ldo,
                                 const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s) {
-  hipLaunchKernelGGL(splitk_combine_norm_kernel, dim3(M), dim3(256), 0, s, part, kc, M, N, ldp, resid, ldo,
-                     normw, eps, xn, ldn);
+  static const bool fixed = !(getenv("TTS_COMBINE_FIXED") && !atoi(getenv("TTS_COMBINE_FIXED")));
+  if (fixed && N == 2048 && kc == 4)
+    hipLaunchKernelGGL((splitk_combine_norm_fixed_kernel<4, 1>), dim3(M), dim3(256), 0, s, part, M, ldp, resid, ldo,
+                       normw, eps, xn, ldn);
+  else if (fixed && N == 4096 && kc == 7)
+    hipLaunchKernelGGL((splitk_combine_norm_fixed_kernel<7, 2>), dim3(M), dim3(256), 0, s, part, M, ldp, resid, ldo,
+                       normw, eps, xn, ldn);
+  else
+    hipLaunchKernelGGL(splitk_combine_norm_kernel, dim3(M), dim3(256), 0, s, part, kc, M, N, ldp, resid, ldo,
+                       normw, eps, xn, ldn);
 }
 
 void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
