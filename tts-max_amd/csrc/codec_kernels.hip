@@ -197,16 +197,21 @@ static void launch_split(GemmF32Args g, int target, hipStream_t s) {
 // accumulation (v_mfma_f32_32x32x16_bf16, smallest terms first); the dropped terms are
 // <= 2^-24 relative, i.e. fp32 products.  Same tiles, staging order and epilogue as
 // gemm_f32_kernel.
-template <int TM, int TN, bool BPRE>
-__global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
+// Tile TM x TN over WM x WN waves, each wave (TM/WM) x (TN/WN) = MI x NJ accumulators of 32x32.
+// 64x64 and 128x128: 2 x 2 waves (256 threads); 256x128 / 256x256: 4 x 2 / 4 x 4 waves, each
+// 64x64 — half (a quarter) the operand bytes per MAC of the 128x128 tile, one workgroup per CU.
+template <int TM, int TN, int WM, int WN, bool BPRE>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
+  constexpr int NT = 64 * WM * WN;
   constexpr int BK = 32, LS = BK + 8;           // bf16 row stride 80 B
-  constexpr int MI = TM / 64, NJ = TN / 64;     // 32x32 accumulators per wave
-  constexpr int TPA = 256 / TM, KPA = BK / TPA; // A staging: threads per row, floats per thread
-  constexpr int TPB = 256 / TN, KPB = BK / TPB;
+  constexpr int MI = TM / WM / 32, NJ = TN / WN / 32;  // 32x32 accumulators per wave
+  constexpr int TPA = NT / TM, KPA = BK / TPA; // A staging: threads per row, floats per thread
+  constexpr int TPB = NT / TN, KPB = BK / TPB;
+  static_assert(KPA >= 8 && KPA % 8 == 0 && KPB >= 8 && KPB % 8 == 0, "staging: whole 8-element chunks per thread");
   __shared__ __attribute__((aligned(16))) bf16_t Ah[TM * LS], Am[TM * LS], Al[TM * LS];
   __shared__ __attribute__((aligned(16))) bf16_t Bh[TN * LS], Bm[TN * LS], Bl[TN * LS];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int nbn = (g.N + TN - 1) / TN;
   const int m0 = (blockIdx.x / nbn) * TM, n0 = (blockIdx.x % nbn) * TN;
   const int kbeg = blockIdx.y * g.kchunk;
@@ -303,14 +308,14 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
       bf16x8_t ah[MI], am[MI], al[MI], bh[NJ], bm[NJ], bl[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int r = wm * (TM / 2) + i * 32 + (lane & 31);
+        const int r = wm * (TM / WM) + i * 32 + (lane & 31);
         ah[i] = *(const bf16x8_t*)(Ah + r * LS + ko);
         am[i] = *(const bf16x8_t*)(Am + r * LS + ko);
         al[i] = *(const bf16x8_t*)(Al + r * LS + ko);
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int r = wn * (TN / 2) + j * 32 + (lane & 31);
+        const int r = wn * (TN / WN) + j * 32 + (lane & 31);
         bh[j] = *(const bf16x8_t*)(Bh + r * LS + ko);
         bm[j] = *(const bf16x8_t*)(Bm + r * LS + ko);
         bl[j] = *(const bf16x8_t*)(Bl + r * LS + ko);
@@ -346,14 +351,14 @@ __global__ __launch_bounds__(256) void gemm_bx3_kernel(GemmF32Args g) {
   // epilogue (as gemm_f32_kernel): lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int n = n0 + wn * (TN / 2) + j * 32 + (lane & 31);
+    const int n = n0 + wn * (TN / WN) + j * 32 + (lane & 31);
     if (n >= g.N) continue;
     const float bias = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (TM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int m = m0 + wm * (TM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= g.M) continue;
         if (g.ksplit > 1) {
           g.part[((size_t)blockIdx.y * g.M + m) * g.N + n] = acc[i][j][r];
@@ -381,10 +386,21 @@ void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
   const int big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
   if (bx3 && g.K % 32 == 0 && g.lda % 4 == 0) {
     const dim3 g128(big), g64(((g.M + 63) / 64) * ((g.N + 63) / 64));
-    if (g.Bp && big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, true>), g128, dim3(256), 0, s, g);
-    else if (g.Bp) hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, true>), g64, dim3(256), 0, s, g);
-    else if (big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, false>), g128, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, false>), g64, dim3(256), 0, s, g);
+    // TTS_CODEC_TILE: 0 = 128x128; 1 (default) = 256x128, 2 = 128x256 (8 waves of 64x64, one
+    // workgroup per CU: fewer operand bytes per MAC, and with 256 columns each A element is
+    // split for twice the outputs) where those tiles still make >= 2 rounds of the CUs (the
+    // ragged batch's big GEMMs).  (256x256 on 16 waves spills: 4 waves per SIMD leave 128 VGPRs)
+    static const int big_tiles = getenv("TTS_CODEC_TILE") ? atoi(getenv("TTS_CODEC_TILE")) : 1;
+    const int t21 = ((g.M + 255) / 256) * ((g.N + 127) / 128);
+    const int t12 = ((g.M + 127) / 128) * ((g.N + 255) / 256);
+    if (g.Bp && big_tiles == 1 && t21 >= 2 * 256)
+      hipLaunchKernelGGL((gemm_bx3_kernel<256, 128, 4, 2, true>), dim3(t21), dim3(512), 0, s, g);
+    else if (g.Bp && big_tiles == 2 && t12 >= 2 * 256)
+      hipLaunchKernelGGL((gemm_bx3_kernel<128, 256, 2, 4, true>), dim3(t12), dim3(512), 0, s, g);
+    else if (g.Bp && big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, 2, 2, true>), g128, dim3(256), 0, s, g);
+    else if (g.Bp) hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, 2, 2, true>), g64, dim3(256), 0, s, g);
+    else if (big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, 2, 2, false>), g128, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, 2, 2, false>), g64, dim3(256), 0, s, g);
     return;
   }
   if (big >= 256) launch_split<128, 128>(g, 0, s);
