@@ -239,11 +239,13 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.gran.alloc((size_t)(QKV + H * D) / 2 * 8);  // q|k|v granules, then the attention row's
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
-  {  // batched decode attention: chunks of ~128 positions (4 waves x 32) over the longest
-     // context, 2..16 per (row, kv head); TTS_ATTN_SPLIT=<n> forces n (<= 1: one workgroup)
+  {  // batched decode attention split over the context (flash-decoding chunks + merge kernel,
+     // lm_attn.hip): measured slower than one workgroup per (row, kv head) at TTS-1's 8 and 32
+     // rows (8.8 -> 10.4-11.2 us, 9.4 -> 17.1-17.8 us; profiles/r4c_ab_split*.txt) and at
+     // TTS-1-Max's 8 rows (12.0 -> 9.0 + 5.0 us merge, profiles/r4c_tts1max_bs8_kernel_stats.csv),
+     // so off by default; TTS_ATTN_SPLIT=<n>: n chunks per (row, kv head)
     const char* ev = getenv("TTS_ATTN_SPLIT");
-    int ns = std::min(16, std::max(2, (S + 127) / 128));
-    if (ev) ns = std::min(16, atoi(ev));
+    int ns = ev ? std::min(16, atoi(ev)) : 1;
     w.attn_splits = ns;
     if (ns > 1) w.apart.alloc((size_t)B * KVH * ns * (8 + 4 * D) * 4);
   }

@@ -148,11 +148,12 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   static const bool agr_on = !(getenv("TTS_AGR") && !atoi(getenv("TTS_AGR")));
   if (agr_on && M <= 16 && epi == EPI_RESID && !p.a_lds && p.sp.kc > 1 && p.grid * p.sp.kc > 2 * num_cu)
     return p;  // a_lds = false, unsliced
-  // 17..32 rows, K in one chunk, plain store / residual (TTS-1 qkv, o_proj): every workgroup
-  // would stage all 32 A rows (128 KiB) into LDS although each wave reads only its own K
-  // range; instead each wave loads its A fragments beside its weight tiles (A_GLOBAL ring, L2
-  // hits).  TTS_AGR32=0: LDS staging (experiment hook)
-  static const bool agr32 = !(getenv("TTS_AGR32") && !atoi(getenv("TTS_AGR32")));
+  // 17..32 rows, K in one chunk, plain store / residual (TTS-1 qkv, o_proj): each wave loading
+  // its own A fragments beside its weight tiles (A_GLOBAL ring, L2 hits) instead of every
+  // workgroup staging all 32 A rows (128 KiB) into LDS — measured slower (qkv 10.6 -> 15.5 us,
+  // o_proj 8.7 -> 12.0 us, bs=32 step 1.21 -> 1.36 ms; profiles/r4c_ab_agr32.txt: the
+  // fragment-shaped L2 loads cost more than the full-line LDS-DMA).  Experiment hook TTS_AGR32=1
+  static const bool agr32 = getenv("TTS_AGR32") && atoi(getenv("TTS_AGR32"));
   bool agr_rows32 = false;
   if (agr32 && M > 16 && M <= 32 && p.sp.kc == 1 && (epi == EPI_STORE || epi == EPI_RESID) && p.sp.ku <= 2) {
     p.a_lds = false;
