@@ -309,6 +309,10 @@ bool use_fused_oproj() {
 
 // 17..32 rows: RMSNorm in the GEMM's LDS prologue (rows landed by LDS-DMA, a wave per row)
 // instead of a standalone launch — experiment hook TTS_NORM32=1 (round 2 measured it slower)
+bool use_kslice32() {
+  static const bool v = !(getenv("TTS_KSLICE32") && !atoi(getenv("TTS_KSLICE32")));
+  return v;
+}
 bool norm_in_lds32() {
   static const bool v = getenv("TTS_NORM32") && atoi(getenv("TTS_NORM32"));
   return v;
@@ -372,6 +376,30 @@ struct Ctx {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
+      }
+      // 17..32 rows of qkv / o_proj (kc = 1, K 2048): K split over 4 workgroups (each stages a
+      // quarter of the A rows, 32 KiB instead of 128) + a combine: plain bf16 rows, or residual
+      // add + the next RMSNorm (the gate/up prologue's norm) in one pass.  TTS_KSLICE32=0: off
+      if (!norm && m > 16 && m <= 32 && K == 2048 && !logit_extra && (epi == EPI_STORE || epi == EPI_RESID) &&
+          use_kslice32() && p.sp.kc == 1 && p.sp.waves == 16 && p.sp.ksplit == 16 && p.sp.ku == 2 && p.sp.ng == 1 &&
+          (size_t)4 * m * ldo * 4 <= w.kpart.bytes) {
+        WgemmArgs a;
+        a.x = xin; a.M = m; a.K = K / 4; a.ldx = K;
+        a.w = W; a.N = N; a.ldo = ldo;
+        a.ur = p.sp.ur(); a.kc = 1;
+        a.part_out = w.kpart.as<float>();
+        a.stamps = stamp_buf();
+        launch_wgemm_kslice(a, N / 16, s);
+        bf16_t* o = out ? out + (size_t)r0 * ldo : nullptr;
+        bf16_t* rs = resid ? resid + (size_t)r0 * ldo : nullptr;
+        if (epi == EPI_RESID && next_norm && rows <= 32) {
+          launch_splitk_combine_norm(w.kpart.as<float>(), 4, m, N, ldo, rs, ldo, next_norm, c.rms_norm_eps,
+                                     w.xn.as<bf16_t>(), ldo, s);
+          pending_norm = next_norm;
+        } else {
+          launch_splitk_combine(w.kpart.as<float>(), 4, m, N, ldo, o, rs, ldo, s);
+        }
+        continue;
       }
       WgemmArgs a;
       if (logit_extra) {
@@ -496,8 +524,9 @@ struct Ctx {
         launch_rope_append(a, s);
         launch_attn_prefill(a, s);
       }
-      if (!foproj)
-        gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID);
+      if (!foproj)  // (decode: o_proj's combine may normalise with ln2 for the gate/up launch)
+        gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID,
+             nullptr, decode ? ly.ln2 : nullptr);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;

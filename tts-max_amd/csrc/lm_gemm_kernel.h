@@ -200,8 +200,11 @@ TTS_DEV void argmax_merge(float& v, int& i, float v2, int i2) {
 constexpr int A_GLOBAL = 0, A_LDS = 1;
 
 // MT_MAX: compile-time bound on 16-row m-tiles (1 for decode, 4 for up to 64 rows)
+// KSW < KSPLIT (K-sliced over workgroups, kc = 1 layouts): a unit's KSPLIT layout k-parts are
+// spread over SL = KSPLIT / KSW workgroups (grid.y), KSW waves each; a.K = the K / SL columns
+// a workgroup stages, fp32 partials of each slice to part_out (summed by a combine kernel).
 template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R,
-          bool EARLY>
+          bool EARLY, int KSW = KSPLIT>
 __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
@@ -227,15 +230,17 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
   }
-  constexpr int UPW = WAVES / KSPLIT;  // units processed concurrently by one workgroup
+  constexpr int UPW = WAVES / KSW;  // units processed concurrently by one workgroup
+  constexpr int SL = KSPLIT / KSW;  // K slices over workgroups (grid.y)
   // this workgroup's index among the GEMM workgroups (the attention ones excluded)
   const int bx = (FATT && a.fattn_wgs && a.fattn_first) ? (int)blockIdx.x - a.fattn_wgs : (int)blockIdx.x;
   unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
   TTS_STAMP(stp, 0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int kpart = wave % KSPLIT;
-  const int ugrp = wave / KSPLIT;
+  const int kq = wave % KSW;  // k-part within the workgroup (split-K combine through LDS)
+  const int kpart = (SL > 1 ? (int)blockIdx.y * KSW : 0) + kq;  // k-part of the layout
+  const int ugrp = wave / KSW;
   const int M = a.M;
   const int mtn = (M + 15) >> 4;
   // column split (a.csplit = 2, store / residual epilogues): work unit u is half u & 1 of
@@ -249,13 +254,13 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // chunk; its stage st covers k-tiles kt(st) .. +KU-1 of chunk st / Sc.  K-sliced launches
   // (a.sliced) run chunk blockIdx.y only: a.K = one chunk, A = that chunk's columns.
   const int kc = a.kc;
-  const int KT = a.sliced ? (a.K >> 5) * kc : (a.K >> 5);  // k-tiles of the whole matrix
+  const int KT = a.sliced ? (a.K >> 5) * kc : (a.K >> 5) * SL;  // k-tiles of the whole matrix
   const int KTc = KT / kc;
   const int kt_pc = KTc / KSPLIT;
   const int Sc = kt_pc / KU;
   const int st_off = a.sliced ? blockIdx.y * Sc : 0;        // first (layout) stage of this launch
-  const int kt_base = a.sliced ? blockIdx.y * KTc : 0;      // first k-tile held in A
-  const bf16_t* xg = a.x ? a.x + (a.sliced ? (size_t)blockIdx.y * a.K : 0) : nullptr;
+  const int kt_base = a.sliced ? blockIdx.y * KTc : (SL > 1 ? (int)blockIdx.y * (a.K >> 5) : 0);  // first k-tile in A
+  const bf16_t* xg = a.x ? a.x + ((a.sliced || SL > 1) ? (size_t)blockIdx.y * a.K : 0) : nullptr;
   const int ldxs = a.K + 8;  // +16 B per row: the 16 A rows land on distinct LDS bank slots
   const int ustride = nproj * UPW;  // (the fused launch's attention / o_proj workgroups excluded)
 
@@ -596,13 +601,13 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       continue;
     }
     // ---- split-K combine through LDS, fixed order (deterministic)
-    if constexpr (KSPLIT > 1) {
-      // slot of wave (ugrp, kpart > 0): ugrp * (KSPLIT-1) + kpart - 1
+    if constexpr (KSW > 1) {
+      // slot of wave (ugrp, kq > 0): ugrp * (KSW-1) + kq - 1
       constexpr int PS = NG * MT_MAX * 4 * 64;
       // one 16-B LDS access per (tile, lane): the sums (fixed order, p ascending) are the
-      // same as element-wise, and the KSPLIT - 1 reads of a lane are all in flight at once
-      if (kpart > 0) {
-        float* myred = red + (size_t)(ugrp * (KSPLIT - 1) + kpart - 1) * PS;
+      // same as element-wise, and up to 16 reads of a lane are in flight at once
+      if (kq > 0) {
+        float* myred = red + (size_t)(ugrp * (KSW - 1) + kq - 1) * PS;
 #pragma unroll
         for (int g = 0; g < NG; ++g)
 #pragma unroll
@@ -611,33 +616,47 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
       lds_barrier();
       if (first) TTS_STAMP(stp, 4);
-      if (kpart == 0) {
-        constexpr int NPV = (KSPLIT - 1) * NG * MT_MAX;
+      if (kq == 0) {
+        constexpr int NPV = (KSW - 1) * NG * MT_MAX;
         if constexpr (NPV <= 16) {  // every partial read issued before the first add
-          f32x4_t pv[KSPLIT > 1 ? KSPLIT - 1 : 1][NG][MT_MAX];
+          f32x4_t pv[KSW > 1 ? KSW - 1 : 1][NG][MT_MAX];
 #pragma unroll
-          for (int p = 1; p < KSPLIT; ++p)
+          for (int p = 1; p < KSW; ++p)
 #pragma unroll
             for (int g = 0; g < NG; ++g)
 #pragma unroll
               for (int mt = 0; mt < MT_MAX; ++mt)
-                pv[p - 1][g][mt] = *(const f32x4_t*)(red + (size_t)(ugrp * (KSPLIT - 1) + p - 1) * PS +
+                pv[p - 1][g][mt] = *(const f32x4_t*)(red + (size_t)(ugrp * (KSW - 1) + p - 1) * PS +
                                                      ((g * MT_MAX + mt) * 64 + lane) * 4);
 #pragma unroll
-          for (int p = 1; p < KSPLIT; ++p)
+          for (int p = 1; p < KSW; ++p)
 #pragma unroll
             for (int g = 0; g < NG; ++g)
 #pragma unroll
               for (int mt = 0; mt < MT_MAX; ++mt) acc[g][mt] += pv[p - 1][g][mt];
         } else {
+          // batches of HB k-parts, each batch's reads in flight before its adds (p ascending;
+          // rows past M read duplicates, never stored: no per-tile branch around a read)
+          constexpr int HB = 8 / (NG * MT_MAX) > 0 ? 8 / (NG * MT_MAX) : 1;
 #pragma unroll
-          for (int p = 1; p < KSPLIT; ++p) {
-            const float* o = red + (size_t)(ugrp * (KSPLIT - 1) + p - 1) * PS;
+          for (int p0 = 1; p0 < KSW; p0 += HB) {
+            f32x4_t pv[HB][NG][MT_MAX];
 #pragma unroll
-            for (int g = 0; g < NG; ++g)
+            for (int j = 0; j < HB; ++j)
 #pragma unroll
-              for (int mt = 0; mt < MT_MAX; ++mt)
-                if (mt < mtn) acc[g][mt] += *(const f32x4_t*)(o + ((g * MT_MAX + mt) * 64 + lane) * 4);
+              for (int g = 0; g < NG; ++g)
+#pragma unroll
+                for (int mt = 0; mt < MT_MAX; ++mt)
+                  if (p0 + j < KSW)
+                    pv[j][g][mt] = *(const f32x4_t*)(red + (size_t)(ugrp * (KSW - 1) + p0 + j - 1) * PS +
+                                                     ((g * MT_MAX + mt) * 64 + lane) * 4);
+#pragma unroll
+            for (int j = 0; j < HB; ++j)
+#pragma unroll
+              for (int g = 0; g < NG; ++g)
+#pragma unroll
+                for (int mt = 0; mt < MT_MAX; ++mt)
+                  if (p0 + j < KSW) acc[g][mt] += pv[j][g][mt];
           }
         }
       }
@@ -646,7 +665,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
 
     // ---- epilogue (lane owns column n, rows m = mt*16 + 4*(lane>>4) + r)
-    if (kpart == 0 && active && (!cs2 || ((lane >> 3) & 1) == (u & 1))) {
+    if (kq == 0 && active && (!cs2 || ((lane >> 3) & 1) == (u & 1))) {
       const int n = (u >> cs2) * 16 + (lane & 15);
 #pragma unroll
       for (int mt = 0; mt < MT_MAX; ++mt) {
@@ -679,7 +698,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
     if constexpr (FATT) {  // publish the unit's 16 columns of row 0 as 8 granules
-      if (kpart == 0 && active && a.fattn_wgs) {
+      if (kq == 0 && active && a.fattn_wgs) {
         const uint32_t mine = (uint32_t)f2bf(acc[0][0][0]);
         const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
         if (lane < 16 && !(lane & 1)) {
@@ -721,7 +740,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     float* rv = red;
     int* ri = (int*)(red + UPW * MT_MAX * 16);
     lds_barrier();
-    if (kpart == 0 && (lane & 15) == 0) {
+    if (kq == 0 && (lane & 15) == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT_MAX; ++mt)
 #pragma unroll

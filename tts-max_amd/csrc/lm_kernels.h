@@ -168,6 +168,9 @@ inline size_t wgemm_part_elems(const WgemmPlan& p, int M, int ldo) {
 bool wgemm_supported(int M, int N, int K, int epi);
 bool wgemm_fattn_ok(int N, int K, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
+// 17..32 rows of a kc = 1 qkv / o_proj layout (16-wave KSPLIT 16, KU 2), K split over 4
+// workgroups (grid.y): fp32 partials [4][M][ldo] to a.part_out; a.K = K / 4 (lm_gemm_store.hip)
+void launch_wgemm_kslice(const WgemmArgs& a, int units, hipStream_t s);
 
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
 // MFMA blocks; epilogues EPI_STORE / EPI_RESID / EPI_SWIGLU; no fused RMSNorm
