@@ -9,6 +9,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 cp $O/long_tf_dev_lm_tts1_long.json $O/${T}_long_tf_dev_lm_tts1_long.json && \
 timeout -k 10 600 python scripts/env_ab_probe.py TTS_KSLICE32 32 2 > $O/${T}_ab_kslice32.txt 2>&1 && \
 timeout -k 10 600 python scripts/env_ab_probe.py TTS_KSLICE32 24 1 > $O/${T}_ab_kslice24.txt 2>&1 && \
+timeout -k 10 600 python scripts/env_ab_probe.py TTS_QKV_DEFER 32 2 > $O/${T}_ab_qkvdefer32.txt 2>&1 && \
 timeout -k 10 900 python bench.py --no-cpu-baseline > $O/${T}_bench.json 2> $O/${T}_bench.err
 rc=$?
 echo "rc=$rc"

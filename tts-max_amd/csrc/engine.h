@@ -88,6 +88,7 @@ struct LmWork {
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
   DevBuf apart;                                     // split decode attention partials (AttnArgs::part)
   int attn_splits = 0;                              // chunks per (row, kv head) of the batched decode attention
+  bool attn_splits_on() const { return attn_splits > 1; }
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]

@@ -80,14 +80,33 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
   const bf16_t* qrow = a.qkv + (size_t)row * a.ld_qkv;
   const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
   const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
+  // the group's q | k | v: columns of the qkv row, or sums of a K-sliced launch's partials
+  __shared__ __attribute__((aligned(16))) bf16_t raw[DEC_G * D + 2 * D];
+  const bf16_t* qsrc = qrow + kvh * DEC_G * D;
+  const bf16_t* ksrc = qrow + a.H * D + kvh * D;
+  const bf16_t* vsrc = qrow + a.H * D + a.KVH * D + kvh * D;
+  if (a.qkv_part) {
+    for (int i = tid; i < DEC_G * D + 2 * D; i += NW * 64) {
+      const int col = i < DEC_G * D ? kvh * DEC_G * D + i
+                    : (i < DEC_G * D + D ? a.H * D + kvh * D + i - DEC_G * D
+                                         : a.H * D + a.KVH * D + kvh * D + i - DEC_G * D - D);
+      float v = 0.f;
+      for (int sl = 0; sl < a.qkv_nsl; ++sl) v += a.qkv_part[((size_t)sl * a.rows + row) * a.ld_qkv + col];
+      raw[i] = f2bf(v);
+    }
+    lds_barrier();
+    qsrc = raw;
+    ksrc = raw + DEC_G * D;
+    vsrc = raw + DEC_G * D + D;
+  }
   for (int i = tid; i < DEC_G * D + D; i += NW * 64) {
     if (i < DEC_G * D) {
       const int g = i / D, d = i % D;
-      qs[i] = rope_at<D>(qrow + (kvh * DEC_G + g) * D, d, cosr, sinr);
+      qs[i] = rope_at<D>(qsrc + g * D, d, cosr, sinr);
     } else {
       const int d = i - DEC_G * D;
-      knew[d] = f2bf(rope_at<D>(qrow + a.H * D + kvh * D, d, cosr, sinr));
-      vnew[d] = qrow[a.H * D + a.KVH * D + kvh * D + d];
+      knew[d] = f2bf(rope_at<D>(ksrc, d, cosr, sinr));
+      vnew[d] = vsrc[d];
     }
   }
   lds_barrier();

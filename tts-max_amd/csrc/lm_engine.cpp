@@ -309,6 +309,10 @@ bool use_fused_oproj() {
 
 // 17..32 rows: RMSNorm in the GEMM's LDS prologue (rows landed by LDS-DMA, a wave per row)
 // instead of a standalone launch — experiment hook TTS_NORM32=1 (round 2 measured it slower)
+bool use_qkv_defer() {
+  static const bool v = !(getenv("TTS_QKV_DEFER") && !atoi(getenv("TTS_QKV_DEFER")));
+  return v;
+}
 bool use_kslice32() {
   static const bool v = !(getenv("TTS_KSLICE32") && !atoi(getenv("TTS_KSLICE32")));
   return v;
@@ -332,6 +336,9 @@ struct Ctx {
   // w.xn holds RMSNorm(w.x, pending_norm) when a residual combine produced it (17..32-row
   // decode: the down projection's K-sliced combine normalises with the next norm weight)
   const bf16_t* pending_norm = nullptr;
+  // 17..32-row decode: the K-sliced QKV launch leaves fp32 partials in w.kpart and the decode
+  // attention sums them (no combine launch); set by layers() around the QKV gemm
+  bool defer_qkv_combine = false, qkv_part_pending = false;
 
   void gemm(const bf16_t* x, int rows, int K, const bf16_t* W, int N, const bf16_t* normw,
             bf16_t* out, int ldo, bf16_t* resid, int epi, const WgemmArgs* logit_extra = nullptr,
@@ -392,7 +399,9 @@ struct Ctx {
         launch_wgemm_kslice(a, N / 16, s);
         bf16_t* o = out ? out + (size_t)r0 * ldo : nullptr;
         bf16_t* rs = resid ? resid + (size_t)r0 * ldo : nullptr;
-        if (epi == EPI_RESID && next_norm && rows <= 32) {
+        if (epi == EPI_STORE && defer_qkv_combine) {  // the decode attention sums the partials
+          qkv_part_pending = true;
+        } else if (epi == EPI_RESID && next_norm && rows <= 32) {
           launch_splitk_combine_norm(w.kpart.as<float>(), 4, m, N, ldo, rs, ldo, next_norm, c.rms_norm_eps,
                                      w.xn.as<bf16_t>(), ldo, s);
           pending_norm = next_norm;
@@ -449,6 +458,10 @@ struct Ctx {
     if (decode && rows > 1 && w.attn_splits > 1) {  // (one row: the fused launch's single-workgroup form)
       a.splits = w.attn_splits;
       a.part = w.apart.as<float>();
+    }
+    if (decode && qkv_part_pending) {
+      a.qkv_part = w.kpart.as<float>();
+      a.qkv_nsl = 4;
     }
     return a;
   }
@@ -512,8 +525,14 @@ struct Ctx {
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE, &fx);
       } else {
+        // (defer: TTS_QKV_DEFER=0 keeps the combine launch)
+        defer_qkv_combine = decode && rows > 16 && rows <= 32 && use_qkv_defer() && !w.attn_splits_on();
+        qkv_part_pending = false;
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE);
+        defer_qkv_combine = false;
+        if (qkv_part_pending) a = attn_args(l, rows, slot, pos, decode);
+        qkv_part_pending = false;
       }
       // attention output (bf16 rows of w.attn_out): inside the QKV launch (one-row step), one
       // workgroup per (row, kv head) (decode), or per query block x kv head (prefill)

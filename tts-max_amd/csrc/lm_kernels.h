@@ -63,6 +63,10 @@ struct AttnArgs {
   // splits <= 1: one workgroup per (row, kv head)
   int splits = 0;
   float* part = nullptr;  // [rows][KVH][splits][2*4 + 4*D] fp32
+  // decode: q | k | v as fp32 partials of a K-sliced QKV launch ([qkv_nsl][rows][ld_qkv], summed
+  // in slice order and rounded to bf16 here, as splitk_combine_kernel would) instead of qkv
+  const float* qkv_part = nullptr;
+  int qkv_nsl = 0;
 };
 
 // ---- sampling / bookkeeping state of a decode step (lm_ops.hip, lm_finalize.h)
