@@ -56,6 +56,7 @@ struct Codec {
   DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
   DevBuf meta;   // segment tables, wave offsets, code rows, attention query blocks
   DevBuf planes;  // every GEMM weight (B operand) split once into its bf16 h / m / l planes
+  DevBuf aplanes;  // TTS_CODEC_APRE: the current GEMM's A operand split into planes
   DevBuf rope_cs;  // [heads][32][cos, sin] of the attention's RoPE
   std::map<const float*, const uint16_t*> bplanes;
   DevBuf codes, wav;  // all utterances' codes; host-bound waveforms staged on the device
@@ -303,7 +304,7 @@ void codec_load(Engine* e, const tts_codec_config* cfgp, const tts_tensor_desc* 
 
 namespace {
 
-thread_local const Codec* t_codec = nullptr;  // the codec whose pass is being enqueued
+thread_local Codec* t_codec = nullptr;  // the codec whose pass is being enqueued
 
 void gemm(const float* A, int M, int K, int lda, const float* B, int N, const float* bias,
           float* C, int ldc, const float* resid, int act, hipStream_t s) {
@@ -312,6 +313,16 @@ void gemm(const float* A, int M, int K, int lda, const float* B, int N, const fl
   auto it = t_codec->bplanes.find(B);
   if (it != t_codec->bplanes.end()) g.Bp = it->second;
   g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
+  // experiment hook TTS_CODEC_APRE=1: A split into its bf16 planes by one pass, shared by every
+  // N tile of the big GEMMs (instead of each workgroup splitting its A tiles while staging)
+  static const bool apre = getenv("TTS_CODEC_APRE") && atoi(getenv("TTS_CODEC_APRE"));
+  if (apre && g.Bp && M >= 4096 && K % 32 == 0 && lda % 8 == 0) {
+    const long long span = (long long)(M - 1) * lda + K;
+    if (t_codec->aplanes.bytes < (size_t)span * 6) t_codec->aplanes.alloc((size_t)span * 6);
+    launch_split_planes(A, t_codec->aplanes.as<uint16_t>(), span, s);
+    g.Ap = t_codec->aplanes.as<uint16_t>();
+    g.ap_plane = span;
+  }
   launch_gemm_f32(g, s);
 }
 

@@ -20,6 +20,10 @@ struct GemmF32Args {
   int M = 0, K = 0, lda = 0;
   const float* B = nullptr;
   const uint16_t* Bp = nullptr;  // optional: B split into bf16 planes [3][N][K] (launch_split_planes)
+  // optional: A split into bf16 planes with A's addressing (element (m, k) of plane p at
+  // Ap + p * ap_plane + m * lda + k; Ap stands for A's own base)
+  const uint16_t* Ap = nullptr;
+  long long ap_plane = 0;
   int N = 0;
   const float* bias = nullptr;
   float* C = nullptr;

@@ -200,7 +200,7 @@ static void launch_split(GemmF32Args g, int target, hipStream_t s) {
 // Tile TM x TN over WM x WN waves, each wave (TM/WM) x (TN/WN) = MI x NJ accumulators of 32x32.
 // 64x64 and 128x128: 2 x 2 waves (256 threads); 256x128 / 256x256: 4 x 2 / 4 x 4 waves, each
 // 64x64 — half (a quarter) the operand bytes per MAC of the 128x128 tile, one workgroup per CU.
-template <int TM, int TN, int WM, int WN, bool BPRE>
+template <int TM, int TN, int WM, int WN, bool BPRE, bool APRE = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = 32, LS = BK + 8;           // bf16 row stride 80 B
@@ -221,6 +221,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
   const int ar = m0 + arow, br = n0 + brow;
   const bool aok = ar < g.M, bok = br < g.N;
   const float* ap = g.A + (size_t)(aok ? ar : g.M - 1) * g.lda + kbeg + ak;
+  // APRE: A already split into its planes (one pass per GEMM input, shared by every N tile)
+  const bf16_t* aq = APRE ? (const bf16_t*)g.Ap + (size_t)(aok ? ar : g.M - 1) * g.lda + kbeg + ak : nullptr;
   const float* bp = g.B + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk;
   // BPRE: B already split into its h / m / l planes (weights, split once at load)
   const bf16_t* bq = BPRE ? (const bf16_t*)g.Bp + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk : nullptr;
@@ -239,14 +241,25 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
   // (unconditional, step index clamped: exact vmcnt waits)
   const int nsteps = (kend - kbeg) / BK;
   constexpr int RB = BPRE ? 1 : KPB / 4, RQ = BPRE ? KPB / 8 : 1;
-  float4 ra[2][KPA / 4], rb[2][RB];
-  u32x4_t rq[2][3][RQ];
-  auto load = [&](int st, float4 (&xa)[KPA / 4], float4 (&xb)[RB], u32x4_t (&xq)[3][RQ]) {
+  constexpr int RA = APRE ? 1 : KPA / 4, RAQ = APRE ? KPA / 8 : 1;
+  float4 ra[2][RA], rb[2][RB];
+  u32x4_t rq[2][3][RQ], raq[2][3][RAQ];
+  auto load = [&](int st, float4 (&xa)[RA], float4 (&xb)[RB], u32x4_t (&xq)[3][RQ], u32x4_t (&xaq)[3][RAQ]) {
     const int kn = min(st, nsteps - 1) * BK;
+    if constexpr (APRE) {
 #pragma unroll
-    for (int v = 0; v < KPA / 4; ++v) {
-      const float4 l = *(const float4*)(ap + kn + 4 * v);
-      xa[v] = aok ? l : z4;
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int v = 0; v < RAQ; ++v) {
+          const u32x4_t l = *(const u32x4_t*)(aq + pl * g.ap_plane + kn + 8 * v);
+          xaq[pl][v] = aok ? l : zq;
+        }
+    } else {
+#pragma unroll
+      for (int v = 0; v < KPA / 4; ++v) {
+        const float4 l = *(const float4*)(ap + kn + 4 * v);
+        xa[v] = aok ? l : z4;
+      }
     }
     if constexpr (BPRE) {
 #pragma unroll
@@ -282,11 +295,21 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
     *(u32x4_t*)mp = m;
     *(u32x4_t*)lp = l;
   };
-  auto stage = [&](const float4 (&xa)[KPA / 4], const float4 (&xb)[RB], const u32x4_t (&xq)[3][RQ]) {
+  auto stage = [&](const float4 (&xa)[RA], const float4 (&xb)[RB], const u32x4_t (&xq)[3][RQ],
+                   const u32x4_t (&xaq)[3][RAQ]) {
+    if constexpr (APRE) {
 #pragma unroll
-    for (int v = 0; v < KPA / 8; ++v)
-      split8(xa[2 * v], xa[2 * v + 1], Ah + arow * LS + ak + 8 * v, Am + arow * LS + ak + 8 * v,
-             Al + arow * LS + ak + 8 * v);
+      for (int v = 0; v < RAQ; ++v) {
+        *(u32x4_t*)(Ah + arow * LS + ak + 8 * v) = xaq[0][v];
+        *(u32x4_t*)(Am + arow * LS + ak + 8 * v) = xaq[1][v];
+        *(u32x4_t*)(Al + arow * LS + ak + 8 * v) = xaq[2][v];
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < KPA / 8; ++v)
+        split8(xa[2 * v], xa[2 * v + 1], Ah + arow * LS + ak + 8 * v, Am + arow * LS + ak + 8 * v,
+               Al + arow * LS + ak + 8 * v);
+    }
     if constexpr (BPRE) {
 #pragma unroll
       for (int v = 0; v < RQ; ++v) {
@@ -334,18 +357,18 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
         }
     }
   };
-  load(0, ra[0], rb[0], rq[0]);
-  load(1, ra[1], rb[1], rq[1]);
+  load(0, ra[0], rb[0], rq[0], raq[0]);
+  load(1, ra[1], rb[1], rq[1], raq[1]);
   for (int st = 0; st < nsteps; st += 2) {
     __syncthreads();
-    stage(ra[0], rb[0], rq[0]);
+    stage(ra[0], rb[0], rq[0], raq[0]);
     __syncthreads();
-    load(st + 2, ra[0], rb[0], rq[0]);
+    load(st + 2, ra[0], rb[0], rq[0], raq[0]);
     compute();
     __syncthreads();
-    stage(ra[1], rb[1], rq[1]);  // (an odd last step stages a clamped duplicate, not computed)
+    stage(ra[1], rb[1], rq[1], raq[1]);  // (an odd last step stages a clamped duplicate, not computed)
     __syncthreads();
-    load(st + 3, ra[1], rb[1], rq[1]);
+    load(st + 3, ra[1], rb[1], rq[1], raq[1]);
     if (st + 1 < nsteps) compute();
   }
   // epilogue (as gemm_f32_kernel): lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -393,7 +416,11 @@ void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
     static const int big_tiles = getenv("TTS_CODEC_TILE") ? atoi(getenv("TTS_CODEC_TILE")) : 1;
     const int t21 = ((g.M + 255) / 256) * ((g.N + 127) / 128);
     const int t12 = ((g.M + 127) / 128) * ((g.N + 255) / 256);
-    if (g.Bp && big_tiles == 1 && t21 >= 2 * 256)
+    if (g.Bp && g.Ap && big_tiles == 1 && t21 >= 2 * 256)
+      hipLaunchKernelGGL((gemm_bx3_kernel<256, 128, 4, 2, true, true>), dim3(t21), dim3(512), 0, s, g);
+    else if (g.Bp && g.Ap && big >= 256)
+      hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, 2, 2, true, true>), g128, dim3(256), 0, s, g);
+    else if (g.Bp && big_tiles == 1 && t21 >= 2 * 256)
       hipLaunchKernelGGL((gemm_bx3_kernel<256, 128, 4, 2, true>), dim3(t21), dim3(512), 0, s, g);
     else if (g.Bp && big_tiles == 2 && t12 >= 2 * 256)
       hipLaunchKernelGGL((gemm_bx3_kernel<128, 256, 2, 4, true>), dim3(t12), dim3(512), 0, s, g);
