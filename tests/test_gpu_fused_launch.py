@@ -95,3 +95,35 @@ def test_fused_wait_timeout_raises_at_first_read():
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines()[-1] == "RAISED", r.stdout
+
+
+_ROWS_CHILD = r'''
+import hashlib, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
+from tts_amd import configs
+from tts_amd.speechlm import MI355XSpeechLM
+arch = configs.LM_ARCHS[sys.argv[2]]
+rows, L, n_last = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+m = MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=rows, max_seq_len=L + 8)
+rng = np.random.default_rng(rows)
+seqs = [rng.integers(0, arch.vocab_size, L - 7 * r).tolist() for r in range(rows)]
+idx = rng.integers(0, arch.vocab_size, (rows, n_last, 64)).astype(np.int32)
+out = m.score_decode(seqs, n_last, idx).numpy()
+print(hashlib.md5(out.tobytes()).hexdigest(), float(np.abs(out).max()))
+'''
+
+
+@pytest.mark.parametrize("arch,rows,L,n_last", [("tts1", 8, 1100, 24), ("tts1-max-2l", 8, 600, 24)])
+def test_batched_fused_qkv_attention_equals_separate_launches(arch, rows, L, n_last):
+    """2..16-row decode steps with the attention carried by the QKV launch (the attention
+    workgroups after the projection's, one per (row, kv head), waiting on each row's tagged
+    granules) give the same bits as the separate QKV and attention launches (TTS_FATTN_ROWS=0),
+    at contexts past the attention's first pass (1,024 positions at head dim 64, 512 at 128)."""
+    outs = {}
+    for v in ("16", "0"):
+        r = subprocess.run([sys.executable, "-c", _ROWS_CHILD, ROOT, arch, str(rows), str(L), str(n_last)],
+                           env=dict(os.environ, TTS_FATTN_ROWS=v), capture_output=True, text=True, timeout=200)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[v] = r.stdout.strip().splitlines()[-1]
+    assert outs["16"] == outs["0"], outs

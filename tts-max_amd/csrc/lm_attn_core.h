@@ -38,12 +38,13 @@ struct DecShape {
 };
 
 constexpr int DEC_G = 4;  // q heads per kv head (GQA 4:1, TTS-1 and TTS-1-Max)
-// Decode workgroup geometry: DEC_NW waves of dec_pw positions each per pass (head dim 64: 16
-// waves x 64 = 1024 positions; 128: 8 waves x 64 = 512, the waves' fragments need 2x the
-// registers, so half the waves per CU)
+// Decode workgroup geometry: DEC_NW = 16 waves of dec_pw positions each per pass (head dim 64:
+// 64 positions, 1,024 per pass; 128: 32 positions, 512 per pass — the fragments of a position
+// are twice as wide, so half the positions keep the registers of the D = 64 wave).  Standalone
+// and fused (QKV launch) attention share the geometry, hence the bits.
 constexpr int DEC_NW = 16;
-template <int D> constexpr int dec_nw() { return D == 64 ? 16 : 8; }
-template <int D> constexpr int dec_pw() { return 64; }
+template <int D> constexpr int dec_nw() { return 16; }
+template <int D> constexpr int dec_pw() { return D == 64 ? 64 : 32; }
 
 // position of A row `row` of m-tile mt (see pi above)
 TTS_DEV int dec_pos(int base, int mt, int row) {

@@ -236,7 +236,9 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.act.alloc((size_t)R * FF * 2);
   w.last_x.alloc((size_t)B * HID * 2);
   w.blocks.alloc(((size_t)R / 16 + B + 1) * 16);  // prefill query blocks: <= rows/16 + one per sequence
-  w.gran.alloc((size_t)(QKV + H * D) / 2 * 8);  // q|k|v granules, then the attention row's
+  // q|k|v granules of every decode row ([B][QKV/2]), and (one-row launches with o_proj fused)
+  // the attention row's at row 1's place (a launch uses one form; every prefill resets them all)
+  w.gran.alloc(((size_t)std::max(B, 2) * QKV + H * D) / 2 * 8);
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
   {  // batched decode attention split over the context (flash-decoding chunks + merge kernel,
@@ -469,9 +471,13 @@ struct Ctx {
   // The one-row decode step's QKV launch carries the attention (TTS-1 geometry: head dim 64);
   // consecutive fused launches differ in (pos, layer)
   bool fused_attn_ok(int rows, bool decode) const {
-    return decode && rows == 1 && use_fused_attn() && c.head_dim == 64 &&
-           c.num_layers >= 2 && c.num_layers <= 64 &&
-           wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
+    if (!decode || !use_fused_attn() || c.num_layers < 2 || c.num_layers > 64) return false;
+    if (rows == 1) return c.head_dim == 64 && wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
+    // 2..16 rows (TTS_FATTN_ROWS = the largest batch that fuses; 0: none): any head dim, the
+    // attention workgroups after the projection's (deadlock-free order), no fused o_proj
+    static const int max_rows = getenv("TTS_FATTN_ROWS") ? atoi(getenv("TTS_FATTN_ROWS")) : 16;
+    static const bool first = getenv("TTS_FATTN_FIRST") && atoi(getenv("TTS_FATTN_FIRST"));
+    return rows <= std::min(16, max_rows) && !first && wgemm_fattn_rows_ok(rows, QKV(), c.hidden_size, c.head_dim, e->num_cu);
   }
   WgemmArgs fused_attn_args(const AttnArgs& a, int layer, bool with_oproj = false) {
     WgemmArgs fx;
@@ -516,7 +522,7 @@ struct Ctx {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
-    const bool foproj = fattn && fused_oproj_ok();
+    const bool foproj = fattn && rows == 1 && fused_oproj_ok();
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
       AttnArgs a = attn_args(l, rows, slot, pos, decode);

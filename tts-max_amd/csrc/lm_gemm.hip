@@ -194,9 +194,17 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
 bool wgemm_fattn_ok(int N, int K, int num_cu) {
   const WgemmPlan p = plan_wgemm(1, N, K, EPI_STORE, num_cu);
   if (!p.a_lds || p.sliced || K > 4096 || p.sp.waves != DEC_NW) return false;  // (16-wave workgroups)
+  if (wgemm_fattn_d(p.sp.ku) != 64) return false;  // (the one-row form: head dim 64)
   const int kch = K / 8, NT = p.sp.waves * 64;
   const int ea = p.sp.waves >= 16 ? 1 : (p.sp.waves >= 8 ? 2 : 4);  // wgemm_ea
   return kch % 64 == 0 && (kch + NT - 1) / NT <= ea;
+}
+
+// 2..16 rows: the QKV launch of the batched step can carry the attention when it is one
+// 16-wave, unsliced launch with the A rows in LDS (any prologue)
+bool wgemm_fattn_rows_ok(int M, int N, int K, int D, int num_cu) {
+  const WgemmPlan p = plan_wgemm(M, N, K, EPI_STORE, num_cu);
+  return M >= 2 && M <= 16 && p.a_lds && !p.sliced && p.sp.waves == DEC_NW && D == wgemm_fattn_d(p.sp.ku);
 }
 
 bool wgemm_supported(int M, int N, int K, int epi) {

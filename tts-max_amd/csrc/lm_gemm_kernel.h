@@ -33,10 +33,12 @@ __host__ __device__ inline int wgemm_red_floats(int waves, int ksplit, int ng, i
 // v until their tag is this launch's, and the attention runs exactly as attn_decode_kernel's
 // (lm_attn_core.h dec_attend: same waves, same order, same bits), writing the group's four
 // heads of the bf16 attention row (fa.out) that o_proj then reads as a plain A row.
-constexpr int FATTN_D = 64;
+// the head dim a fused QKV shape carries (one consumer per instantiation keeps the registers
+// of the other out of it): KU 2 = TTS-1's QKV (K 2048, head dim 64), KU 4 = TTS-1-Max's (K 4096, 128)
+constexpr int wgemm_fattn_d(int ku) { return ku == 2 ? 64 : 128; }
+template <int D>
 constexpr size_t fattn_lds_bytes() {
-  return (size_t)DEC_G * FATTN_D * 4 + (DEC_G * FATTN_D / 2 + FATTN_D) * 4 + 2 * FATTN_D * 2 +
-         (size_t)dec_red_floats<FATTN_D, DEC_NW>() * 4;
+  return (size_t)DEC_G * D * 4 + (DEC_G * D / 2 + D) * 4 + 2 * D * 2 + (size_t)dec_red_floats<D, DEC_NW>() * 4;
 }
 // A bounded granule wait: polls until `ready()` or `spins` polls; on timeout it sets the error
 // flag, and every later wait (this launch or the following ones) that finds the flag set
@@ -55,10 +57,10 @@ TTS_DEV bool fattn_wait(Poll ready, int* err, int spins, bool report) {
   return true;
 }
 
-template <int NT>
+template <int NT, int D>
 TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   static_assert(NT == DEC_NW * 64, "the fused attention runs on 16-wave workgroups");
-  constexpr int D = FATTN_D, PW = dec_pw<D>(), G = DEC_G, H2 = D / 2;
+  constexpr int PW = dec_pw<D>(), G = DEC_G, H2 = D / 2;
   using C = DecShape<D, PW>;
   const AttnArgs& a = wa.fa;
   float* qs = (float*)smem;                   // [G][D] roped q
@@ -203,12 +205,16 @@ constexpr int A_GLOBAL = 0, A_LDS = 1;
 // KSW < KSPLIT (K-sliced over workgroups, kc = 1 layouts): a unit's KSPLIT layout k-parts are
 // spread over SL = KSPLIT / KSW workgroups (grid.y), KSW waves each; a.K = the K / SL columns
 // a workgroup stages, fp32 partials of each slice to part_out (summed by a combine kernel).
+// FROWS: the 2..16-row QKV launch carrying the decode attention (its own instantiation, so the
+// consumer's registers stay out of the plain launches of the same shape)
 template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R,
-          bool EARLY, int KSW = KSPLIT>
+          bool EARLY, int KSW = KSPLIT, bool FROWS = false>
 __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
-  constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && NORM && EARLY && WAVES == DEC_NW;
+  // (one row: the register-staged prologue (EARLY); 2..16 rows (one m-tile): any prologue)
+  constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && WAVES == DEC_NW && KSW == KSPLIT &&
+                        ((EARLY && !FROWS) || (!EARLY && FROWS));
   // fused launch (a.fattn_wgs): the grid's projection / attention / o_proj workgroups
   // (WgemmArgs::fattn_first for the two orders)
   const int fo_wgs = (FATT && a.fattn_wgs && !a.fattn_first) ? a.fo_units : 0;  // o_proj workgroups (order 0)
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     if (a.fattn_wgs) {
       const int cb = a.fattn_first ? (int)blockIdx.x : (int)blockIdx.x - nproj;
       if (cb >= 0 && cb < a.fattn_wgs) {
-        fattn_consumer<NT>(a, smem, cb);
+        fattn_consumer<NT, wgemm_fattn_d(KU)>(a, smem, cb);
         return;
       }
       if (cb >= a.fattn_wgs) {  // (order 0) o_proj unit cb - fattn_wgs
@@ -341,8 +347,16 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
 
   uint32_t ftag = 0;  // fused attention: this launch's granule tag (row 0)
+  uint32_t ftagr[4] = {0u, 0u, 0u, 0u};  // (2..16 rows) the tags of this lane's accumulator rows
   if constexpr (FATT) {
-    if (a.fattn_wgs) ftag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
+    if (a.fattn_wgs) {
+      ftag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
+      if constexpr (!EARLY) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ftagr[r] = ((uint32_t)a.fa.row_pos[min(4 * (lane >> 4) + r, M - 1)] << 6) | (uint32_t)a.fattn_layer;
+      }
+    }
   }
 
   // ---- then the weight stream
@@ -697,14 +711,28 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
     }
-    if constexpr (FATT) {  // publish the unit's 16 columns of row 0 as 8 granules
+    if constexpr (FATT) {  // publish the unit's 16 columns of every row as 8 granules per row
       if (kq == 0 && active && a.fattn_wgs) {
-        const uint32_t mine = (uint32_t)f2bf(acc[0][0][0]);
-        const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
-        if (lane < 16 && !(lane & 1)) {
-          const int n = u * 16 + lane;
-          const uint64_t g = ((uint64_t)ftag << 32) | (other << 16) | mine;
-          __hip_atomic_store(a.gran + n / 2, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (EARLY) {  // (the one-row form: the register-staged prologue, host-checked)
+          const uint32_t mine = (uint32_t)f2bf(acc[0][0][0]);
+          const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+          if (lane < 16 && !(lane & 1)) {
+            const int n = u * 16 + lane;
+            const uint64_t g = ((uint64_t)ftag << 32) | (other << 16) | mine;
+            __hip_atomic_store(a.gran + n / 2, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        } else {  // lane holds rows 4 (lane >> 4) + r of column u * 16 + (lane & 15)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t mine = (uint32_t)f2bf(acc[0][0][r]);
+            const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+            const int m = 4 * (lane >> 4) + r;
+            if (!(lane & 1) && m < M) {
+              const int n = u * 16 + (lane & 15);
+              const uint64_t g = ((uint64_t)ftagr[r] << 32) | (other << 16) | mine;
+              __hip_atomic_store(a.gran + (size_t)m * (a.N / 2) + n / 2, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
         }
       }
     }
@@ -781,18 +809,21 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   const int mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
   lds += (size_t)wgemm_red_floats(WAVES, KSPLIT, NG, mt, a.M, a.K) * sizeof(float);
-  if (a.fattn_wgs) {  // QKV + fused decode attention (one row, D 64, 16-wave workgroups)
-    if (!(EPI == EPI_STORE && ASRC == A_LDS && NORM && a.M == 1 && a.fa.D == FATTN_D && WAVES == DEC_NW &&
-          a.gran && a.fattn_err && !a.sliced))
-      throw std::runtime_error("wgemm: fused attention needs the one-row 16-wave QKV launch (D 64)");
-    if (!EARLY) throw std::runtime_error("wgemm: fused attention needs the register-staged prologue");
+  if (a.fattn_wgs) {  // QKV + fused decode attention (1..16 rows, D 64 / 128, 16-wave workgroups)
+    if (!(EPI == EPI_STORE && ASRC == A_LDS && a.M >= 1 && a.M <= 16 && a.fa.D == wgemm_fattn_d(KU) &&
+          WAVES == DEC_NW && a.gran && a.fattn_err && !a.sliced && a.csplit == 1 && a.fattn_wgs == a.M * a.fa.KVH))
+      throw std::runtime_error("wgemm: fused attention needs a 1..16-row 16-wave QKV launch (D 64 or 128)");
+    if ((a.M == 1) != EARLY)
+      throw std::runtime_error("wgemm: fused attention: one row = the register-staged prologue, 2..16 rows = not");
+    if (a.M > 1 && (a.fattn_first || a.fo_units))
+      throw std::runtime_error("wgemm: multi-row fused attention: producer-first grid order, no fused o_proj");
     if (a.fo_units) {  // fused o_proj: one unit per o_proj (order 1: projection) workgroup, one granule per lane
       const int S = (a.fa.H * a.fa.D / 32) / (KSPLIT * KU);
       if (!(a.fo_w && a.fo_resid && (!a.fattn_first || a.fo_units <= grid) && a.fo_units <= a.fo_ur && S == R &&
             a.fa.H * a.fa.D == KSPLIT * 128 && KSPLIT == WAVES && (size_t)a.M * (a.K + 8) * 2 >= (size_t)KSPLIT * 256))
         throw std::runtime_error("wgemm: fused o_proj shape mismatch");
     }
-    lds = std::max(lds, fattn_lds_bytes());
+    lds = std::max(lds, a.fa.D == 64 ? fattn_lds_bytes<64>() : fattn_lds_bytes<128>());
     grid += a.fattn_wgs + (a.fattn_first ? 0 : a.fo_units);
     if (a.fattn_first) {
       // order 1: the attention workgroups spin on the projection workgroups' granules and
@@ -811,7 +842,11 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
   const dim3 g(grid, a.sliced ? a.kc : 1);
-  if (mt == 1)
+  if (mt == 1 && !EARLY && a.fattn_wgs && a.M > 1) {
+    if constexpr (EPI == EPI_STORE && ASRC == A_LDS && WAVES == DEC_NW)
+      hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, false, KSPLIT, true>), g,
+                         dim3(WAVES * 64), lds, s, a);
+  } else if (mt == 1)
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY>), g,
                        dim3(WAVES * 64), lds, s, a);
   else if (mt == 2)
@@ -827,7 +862,7 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
 template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R>
 static void launch_one(const WgemmArgs& a, int grid, hipStream_t s) {
   bool early = false;
-  if (a.M <= 16) {
+  if (a.M <= 16 && !(a.fattn_wgs && a.M > 1)) {  // (multi-row fused attention: the LDS prologue form)
     const int kch = a.K / 8, NT = WAVES * 64;
     if (ASRC == A_LDS) early = (kch % 64 == 0) && (a.M * kch + NT - 1) / NT <= wgemm_ea(WAVES);
   }

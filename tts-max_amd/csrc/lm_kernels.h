@@ -171,6 +171,7 @@ inline size_t wgemm_part_elems(const WgemmPlan& p, int M, int ldo) {
 }
 bool wgemm_supported(int M, int N, int K, int epi);
 bool wgemm_fattn_ok(int N, int K, int num_cu);
+bool wgemm_fattn_rows_ok(int M, int N, int K, int D, int num_cu);
 void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hipStream_t s);
 // 17..32 rows of a kc = 1 qkv / o_proj layout (16-wave KSPLIT 16, KU 2), K split over 4
 // workgroups (grid.y): fp32 partials [4][M][ldo] to a.part_out; a.K = K / 4 (lm_gemm_store.hip)
