@@ -275,7 +275,8 @@ def main():
         sec["bs32"] = dict(value=round(n32 / reps / e32, 2), unit="audio-codes/s", ms_per_step=round(1000 * e32, 3),
                            x_realtime=round(32 * N / carch.token_rate / e32, 2), lm_prefill_ms=round(a32, 3),
                            lm_decode_ms=round(b32, 3), decode_step_ms=round(b32 / max(k32, 1), 4),
-                           codec_ms=round(codec32_ms, 3), codec_utterances=32, codec_codes_per_utterance=codes_per_utt)
+                           codec_ms=round(codec32_ms, 3), codec_utterances=32, codec_codes_per_utterance=codes_per_utt,
+                           codec_roofline=codec_roofline(carch, codes_per_utt, 32, codec32_ms))
         # the 32-row decode kernels: live HIP-event time, algorithmic bytes, PMC HBM traffic
         k32s = {}
         for k in lm.KERNELS:
@@ -348,6 +349,7 @@ def main():
             "lm_decode_ms": round(lm_decode / args.steps, 3),
             "codec_ms": round(codec_ms, 3),
             "codec_to_host_ms": round(codec_host_ms, 3),
+            "codec_roofline": codec_roofline(carch, codes_per_utt, B, codec_ms),
             "config": {
                 "workload": f"{arch.name} bf16 bs={B}/GPU: prompt {P} tokens ({args.prompt_codes} codes), "
                             f"{N} greedy codes, codec {carch.name} on {codes_per_utt} codes",
@@ -363,6 +365,42 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+CODEC_PRODUCTS = 6  # bf16 MFMA products per fp32 multiply-add in the codec's split-bf16 GEMMs
+
+
+def codec_flops(carch, T):
+    """fp32 FLOPs of Decoder.forward (decoder.py:69-89) on T codes as the engine computes it:
+    FSQ project_out (8 -> vq) + fc_post_a, embed Conv1d(k7), 4 ResnetBlocks (2 Conv1d(k3)),
+    `depth` transformer blocks (c_attn, QK^T and PV over T positions, c_proj, fc1, fc2), each
+    upsampler stage (ConvTranspose1d as a GEMM over every tap, ResnetBlock at the new rate),
+    out_proj, the iSTFT head Linear and the windowed inverse DFT as a basis GEMM."""
+    D, VQ = carch.hidden_dim, carch.vq_dim
+    f = 2.0 * T * 8 * VQ + 2.0 * T * VQ * D + 2.0 * T * 7 * D * D + 4 * 2 * (2.0 * T * 3 * D * D)
+    f += carch.depth * (2.0 * T * D * (3 * D + D + 4 * D + 4 * D) + 4.0 * T * T * D)
+    C, t = D, T
+    for u, k in zip(carch.upsample_factors, carch.kernel_sizes):
+        f += 2.0 * t * C * k * (C // 2)
+        C, t = C // 2, t * u
+        f += 2 * (2.0 * t * 3 * C * C)
+    if carch.upsample_factors:
+        f += 2.0 * t * C * D
+    nfft = 4 * carch.hop_length
+    f += 2.0 * t * D * (nfft + 2) + 2.0 * t * (nfft + 2) * nfft
+    return f
+
+
+def codec_roofline(carch, T, n_utt, ms):
+    """MFMA roofline of a codec pass: fp32-equivalent FLOP/s against the split-bf16 ceiling
+    (dense bf16 MFMA peak / 6 products per fp32 multiply-add)."""
+    fl = codec_flops(carch, T) * n_utt
+    ach = fl / (ms * 1e-3) / 1e12
+    peak = BF16_MFMA_PEAK_TFLOPS / CODEC_PRODUCTS
+    return dict(bound="mfma", achieved=round(ach, 1), peak=round(peak, 1), unit="TFLOP/s (fp32-equivalent)",
+                frac=round(ach / peak, 4), flops=fl, ms=round(ms, 3), utterances=n_utt, codes_per_utterance=T,
+                note="split-bf16 GEMMs: 6 bf16 MFMA products per fp32 multiply-add; peak = 2.5 PF / 6")
 
 
 def synthetic_codes(lm, ids):
