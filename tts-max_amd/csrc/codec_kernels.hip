@@ -671,7 +671,7 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
                                                          const CodecSeg* __restrict__ seg,
                                                          const int2* __restrict__ qblk, int heads,
                                                          const float2* __restrict__ rope_cs,
-                                                         float* __restrict__ out_all) {
+                                                         float* __restrict__ out_all, int expf_mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ks = (bf16_t*)smem;                 // [3][64 keys][APL]
   bf16_t* Vt = Ks + 3 * 64 * APL;             // [3][64 d][APL]
@@ -686,7 +686,11 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
   float* out = out_all + (size_t)seg[qb.x].row * W;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, c16 = lane & 15;
   float* Pw = Ps + wave * 16 * APS;
-  const float scale = 0.125f;  // 1/sqrt(64), exact
+  // softmax in base 2: scores scaled by 1/sqrt(64) * log2(e) once, p = 2^(s - m) on v_exp_f32
+  // (FlashAttention's form; libm expf is a ~20-instruction range reduction, and the softmax's
+  // VALU work, not the MFMAs, bounded this loop).  TTS_CODEC_EXPF=1: expf on s / 8 (round 3)
+  const bool use_expf = expf_mode != 0;
+  const float scale = use_expf ? 0.125f : 0.125f * 1.44269504088896341f;
 
   // Q fragments (A operand, row = query c16 of the wave, d = 32 kk + 8 g + j), split once
   u32x4_t qa[2][3];
@@ -817,12 +821,12 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
       float ps = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const float p = expf(sc[kt][r] - mnew);
+        const float p = use_expf ? expf(sc[kt][r] - mnew) : __builtin_amdgcn_exp2f(sc[kt][r] - mnew);
         Pw[(4 * g + r) * APS + 16 * kt + c16] = p;
         ps += p;
       }
       ps = row16_sum(ps);
-      alpha[r] = expf(mrow[r] - mnew);
+      alpha[r] = use_expf ? expf(mrow[r] - mnew) : __builtin_amdgcn_exp2f(mrow[r] - mnew);
       lrow[r] = lrow[r] * alpha[r] + ps;
       mrow[r] = mnew;
     }
@@ -872,12 +876,13 @@ void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* q
                             int hd, const float* rope_cs, float* out, hipStream_t s) {
   if (hd != AD) throw std::runtime_error("codec attention: head_dim 64 expected");
   dim3 grid(nqblk, heads);
+  static const int expf_mode = getenv("TTS_CODEC_EXPF") ? atoi(getenv("TTS_CODEC_EXPF")) : 0;
   if (attn_waves() == 8)
     hipLaunchKernelGGL(codec_attn_kernel<8>, grid, dim3(512), attn_lds(8), s, qkv, seg, qblk, heads,
-                       (const float2*)rope_cs, out);
+                       (const float2*)rope_cs, out, expf_mode);
   else
     hipLaunchKernelGGL(codec_attn_kernel<4>, grid, dim3(256), attn_lds(4), s, qkv, seg, qblk, heads,
-                       (const float2*)rope_cs, out);
+                       (const float2*)rope_cs, out, expf_mode);
 }
 
 // (cos, sin) of the torchtune rotation for every (head h, pair p): angle h * 10000^(-2p/64),
