@@ -1041,8 +1041,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
   TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
-  TTS_REQUIRE(which < 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention needs one TTS-1 row");
-  TTS_REQUIRE(which != 7 || Ctx(e, e->stream).fused_oproj_ok(), "fused o_proj is off or does not fit");
+  TTS_REQUIRE(which < 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention does not apply to this shape");
+  TTS_REQUIRE(which != 7 || (rows == 1 && Ctx(e, e->stream).fused_oproj_ok()), "fused o_proj: one row, and on");
   hipStream_t s = e->stream;
   Ctx X(e, s);
   const tts_lm_config& c = X.c;
