@@ -83,7 +83,7 @@ for trial in range(2):  # the error is raised at the first read, and again on th
         sys.exit(0)
     except TtsError as e:
         assert "granule wait timed out" in str(e), e
-# the batched step (no fused launch) on the same engine still works
+# the separate-launch step on the same engine still works
 two = m.generate_batch([p, p], **kw)
 assert two[0] == two[1] and len(two[0]) == 64
 print("RAISED")
@@ -91,7 +91,9 @@ print("RAISED")
 
 
 def test_fused_wait_timeout_raises_at_first_read():
-    r = subprocess.run([sys.executable, "-c", _SPIN_CHILD, ROOT], env=dict(os.environ, TTS_FATTN_SPINS="1"),
+    # (TTS_FATTN_ROWS=0: the 2-row batch at the end takes the separate launches)
+    r = subprocess.run([sys.executable, "-c", _SPIN_CHILD, ROOT],
+                       env=dict(os.environ, TTS_FATTN_SPINS="1", TTS_FATTN_ROWS="0"),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines()[-1] == "RAISED", r.stdout
