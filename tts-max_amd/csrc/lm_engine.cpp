@@ -389,7 +389,9 @@ struct Ctx {
       // 17..32 rows of qkv / o_proj (kc = 1, K 2048): K split over 4 workgroups (each stages a
       // quarter of the A rows, 32 KiB instead of 128) + a combine: plain bf16 rows, or residual
       // add + the next RMSNorm (the gate/up prologue's norm) in one pass.  TTS_KSLICE32=0: off
-      if (!norm && m > 16 && m <= 32 && K == 2048 && !logit_extra && (epi == EPI_STORE || epi == EPI_RESID) &&
+      // (chosen by the batch's row count, not the chunk's: a 33..64-row batch runs two chunks,
+      // and every row of a batch must take the same arithmetic)
+      if (!norm && rows > 16 && m <= 32 && K == 2048 && !logit_extra && (epi == EPI_STORE || epi == EPI_RESID) &&
           use_kslice32() && p.sp.kc == 1 && p.sp.waves == 16 && p.sp.ksplit == 16 && p.sp.ku == 2 && p.sp.ng == 1 &&
           (size_t)4 * m * ldo * 4 <= w.kpart.bytes) {
         WgemmArgs a;
@@ -405,7 +407,7 @@ struct Ctx {
           qkv_part_pending = true;
         } else if (epi == EPI_RESID && next_norm && rows <= 32) {
           launch_splitk_combine_norm(w.kpart.as<float>(), 4, m, N, ldo, rs, ldo, next_norm, c.rms_norm_eps,
-                                     w.xn.as<bf16_t>(), ldo, s);
+                                     w.xn.as<bf16_t>() + (size_t)r0 * ldo, ldo, s);
           pending_norm = next_norm;
         } else {
           launch_splitk_combine(w.kpart.as<float>(), 4, m, N, ldo, o, rs, ldo, s);

@@ -11,8 +11,8 @@ void launch_wgemm_store(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipSt
 
 void launch_wgemm_kslice(const WgemmArgs& a_in, int units, hipStream_t s) {
   WgemmArgs a = a_in;
-  if (a.M <= 16 || a.M > 32 || a.K % 512 != 0 || a.kc != 1 || !a.part_out)
-    throw std::runtime_error("wgemm kslice: 17..32 rows, K / 4 a multiple of 512, kc 1, partial workspace");
+  if (a.M < 1 || a.M > 32 || a.K % 512 != 0 || a.kc != 1 || !a.part_out)
+    throw std::runtime_error("wgemm kslice: 1..32 rows, K / 4 a multiple of 512, kc 1, partial workspace");
   a.sliced = 0;
   a.csplit = 1;
   const size_t lds = (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) +
