@@ -378,10 +378,11 @@ struct Ctx {
       // at 17..64 rows every workgroup would normalise every row again — one standalone
       // pass (same canonical order: identical bits) is cheaper, or none when the producer
       // already wrote the normalised rows
-      if (norm && m > 16 && normw == ready && x == w.x.as<bf16_t>()) {
+      // (by the batch's row count: every chunk of a 33..64-row batch takes the same path)
+      if (norm && rows > 16 && normw == ready && x == w.x.as<bf16_t>()) {
         xin = w.xn.as<bf16_t>() + (size_t)r0 * K;
         norm = false;
-      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || (m > 16 && !norm_in_lds32()))) {
+      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || (rows > 16 && !norm_in_lds32()))) {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
