@@ -686,9 +686,8 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
   float* out = out_all + (size_t)seg[qb.x].row * W;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, c16 = lane & 15;
   float* Pw = Ps + wave * 16 * APS;
-  // softmax in base 2: scores scaled by 1/sqrt(64) * log2(e) once, p = 2^(s - m) on v_exp_f32
-  // (FlashAttention's form; libm expf is a ~20-instruction range reduction, and the softmax's
-  // VALU work, not the MFMAs, bounded this loop).  TTS_CODEC_EXPF=1: expf on s / 8 (round 3)
+  // expf_mode 0: softmax in base 2 (scores scaled by 1/sqrt(64) * log2(e) once, p = 2^(s - m) on
+  // v_exp_f32); 1 (default): libm expf on s / 8
   const bool use_expf = expf_mode != 0;
   const float scale = use_expf ? 0.125f : 0.125f * 1.44269504088896341f;
 
@@ -876,7 +875,10 @@ void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* q
                             int hd, const float* rope_cs, float* out, hipStream_t s) {
   if (hd != AD) throw std::runtime_error("codec attention: head_dim 64 expected");
   dim3 grid(nqblk, heads);
-  static const int expf_mode = getenv("TTS_CODEC_EXPF") ? atoi(getenv("TTS_CODEC_EXPF")) : 0;
+  // libm expf by default: the base-2 v_exp_f32 form measured neutral here (32 x 650 codes 62.0 ms
+  // either way, profiles/r4e_ab_codec_expf.txt: the softmax is not what bounds this kernel), so
+  // the reference's exp stays.  TTS_CODEC_EXPF=0: v_exp_f32
+  static const int expf_mode = getenv("TTS_CODEC_EXPF") ? atoi(getenv("TTS_CODEC_EXPF")) : 1;
   if (attn_waves() == 8)
     hipLaunchKernelGGL(codec_attn_kernel<8>, grid, dim3(512), attn_lds(8), s, qkv, seg, qblk, heads,
                        (const float2*)rope_cs, out, expf_mode);
