@@ -227,11 +227,12 @@ def main():
     # + WRITE_SIZE per launch, committed under profiles/), when one exists for this shape
     def pmc(k, rows):
         """(HBM bytes per launch, source file) of kernel k at `rows` rows, or (None, None)."""
-        if arch.name != "tts1":
-            return None, None
         import glob
 
-        hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{k}_{rows}.json")))
+        pre = "" if arch.name == "tts1" else arch.name.replace("-", "") + "_"
+        hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{pre}{k}_{rows}.json")))
+        if arch.name == "tts1":  # (not the other architectures' files)
+            hits = [h for h in hits if os.path.basename(h).split("pmc_")[1].split("_")[0] not in ("tts1max",)]
         if not hits:
             return None, None
         return round(json.load(open(hits[-1]))["hbm_bytes_per_launch"]), os.path.relpath(hits[-1], ROOT)

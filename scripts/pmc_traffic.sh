@@ -3,13 +3,16 @@
 # MI355X_MICROARCH.md (HBM section): one rocprofv3 pass per counter group (FETCH_SIZE and
 # WRITE_SIZE cannot share a pass), FETCH_SIZE doubled on gfx950 (it tallies 128-B streaming
 # requests at 64 B).  Writes gpurun_out/pmc/<kernel>_<rows>.json; copy into profiles/.
-# usage (GPU box): scripts/pmc_traffic.sh [kernel=gate_up] [rows=1]
+# usage (GPU box): [ARCH=tts1-max] scripts/pmc_traffic.sh [kernel=gate_up] [rows=1]
+# (ARCH=tts1-max writes tts1max_<kernel>_<rows>.json)
 set -u
-K=${1:-gate_up}; R=${2:-1}
+K0=${1:-gate_up}; R=${2:-1}
+ARCH=${ARCH:-tts1}
+K=$K0; [ "$ARCH" = "tts1" ] || K=$(echo $ARCH | tr -d '-')_$K0
 OUT=gpurun_out/pmc; mkdir -p $OUT
 export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $OUT/${K}_${R}_$C -o pmc -- \
-    python3 scripts/pmc_probe.py --kernel $K --rows $R --iters 20 > $OUT/${K}_${R}_$C.log 2>&1 || exit $?
+    python3 scripts/pmc_probe.py --arch $ARCH --kernel $K0 --rows $R --iters 20 > $OUT/${K}_${R}_$C.log 2>&1 || exit $?
 done
 python3 scripts/pmc_parse.py $OUT $K $R
