@@ -3,8 +3,8 @@ diagnostic library (make -C tts-max_amd/csrc stamps: -DTTS_STAMPS), runs one lau
 kernel through bench_kernel and prints, per kernel, the workgroups' clock stamps (100 MHz,
 us relative to the earliest entry): entry / after prologue / first unit streamed / first
 unit's epilogue done (GEMM workgroups), entry / granules seen / before attention / after
-attention (fused attention workgroups).  usage: python scripts/stamp_probe.py [CTX] [ROWS]
-(ROWS > 1: the batched kernels; the fused one-row launches are skipped)"""
+attention (fused attention workgroups).  usage: python scripts/stamp_probe.py [CTX] [ROWS] [ARCH]
+(ROWS > 1: the batched kernels, and qkv_attn where the QKV launch carries the attention)"""
 import ctypes
 import os
 import sys
@@ -21,7 +21,8 @@ from tts_amd.speechlm import MI355XSpeechLM  # noqa: E402
 
 ctx = int(sys.argv[1]) if len(sys.argv) > 1 else 450
 rows = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-m = MI355XSpeechLM.synthetic(configs.TTS1, max_batch=rows, max_seq_len=1040)
+arch = configs.LM_ARCHS[sys.argv[3]] if len(sys.argv) > 3 else configs.TTS1
+m = MI355XSpeechLM.synthetic(arch, max_batch=rows, max_seq_len=1040)
 N = 1 << 16
 buf = np.zeros(N, dtype=np.uint64)
 f = lib.tts_debug_stamps
@@ -32,13 +33,13 @@ def q(v):
     return "/".join(f"{x:5.2f}" for x in (np.min(v), np.median(v), np.max(v)))
 
 
-for k in ("qkv", "o_proj", "gate_up", "down", "attention") + (("qkv_attn", "qkv_attn_oproj") if rows == 1 else ()):
+for k in ("qkv", "o_proj", "gate_up", "down", "attention") + (("qkv_attn", "qkv_attn_oproj") if rows == 1 else ("qkv_attn",)):
     for rep in range(3):
         m.bench_kernel(k, rows=rows, ctx=ctx, iters=1)
         assert f(buf.ctypes.data, N) == 0
     t = buf.astype(np.int64)
     if k == "attention":
-        st = t[16384:16384 + rows * 8 * 8].reshape(-1, 8)
+        st = t[16384:16384 + rows * arch.num_kv_heads * 8].reshape(-1, 8)
     else:
         st = t[:16384].reshape(-1, 32)
     st = st[st[:, 0] > 0]
@@ -50,11 +51,10 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention") + (("qkv_attn", "qkv_
         # grid order (WgemmArgs::fattn_first): default projection | attention | o_proj workgroups;
         # TTS_FATTN_FIRST=1: attention first
         first = os.environ.get("TTS_FATTN_FIRST", "0") == "1"
-        nq = 192  # TTS-1 QKV projection workgroups
-        proj, cons = (us[8:], us[:8]) if first else (us[:nq], us[nq:nq + 8])
-        if not first and len(us) > nq + 8:
-            fo = us[nq + 8:]
-            print(f"  o_proj wgs  entry {q(fo[:, 0])}  ({len(fo)} workgroups)")
+        nq = len(us) - rows * arch.num_kv_heads  # projection workgroups (the o_proj ones write no stamps)
+        na = rows * arch.num_kv_heads
+        proj, cons = (us[na:], us[:na]) if first else (us[:nq], us[nq:nq + na])
+
         print(f"  projection  entry {q(proj[:, 0])}  prologue {q(proj[:, 1])}  streamed {q(proj[:, 2])}  epilogue {q(proj[:, 3])}")
         print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  max {q(cons[:, 5])}  pv {q(cons[:, 6])}  attended {q(cons[:, 3])}")
     elif k == "attention":
