@@ -1,7 +1,8 @@
 """Same-box A/B of an engine environment switch (e.g. TTS_AREG, TTS_FUSED_ATTN): per-kernel
 decode times at `rows`, the graph-replayed decode step of a `rows`-utterance batch (500
 codes each) and an md5 of its ids, each setting in its own child process, alternating.
-usage: python scripts/env_ab_probe.py VAR ROWS [ROUNDS]   (settings VAR=0 and VAR=1)"""
+usage: python scripts/env_ab_probe.py VAR ROWS [ROUNDS]   (settings VAR=$AB_V0 (0) and VAR=$AB_V1 (1);
+AB_ARCH: the LM architecture, default tts1)"""
 import os
 import subprocess
 import sys
@@ -13,7 +14,7 @@ sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
 from tts_amd import configs, synth
 from tts_amd.speechlm import MI355XSpeechLM
 rows = int(sys.argv[2])
-arch = configs.TTS1
+arch = configs.LM_ARCHS[os.environ.get("AB_ARCH", "tts1")]
 m = MI355XSpeechLM.synthetic(arch, max_batch=max(rows, 1), max_seq_len=720)
 ks = list(m.KERNELS) + (["qkv_attn"] if rows == 1 and os.environ.get("TTS_FUSED_ATTN", "1") != "0" else [])
 ks += ["qkv_attn_oproj"] if rows == 1 and os.environ.get("TTS_FUSED_ATTN", "1") != "0" and os.environ.get("TTS_FUSED_OPROJ", "1") != "0" else []

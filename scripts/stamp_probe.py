@@ -61,6 +61,9 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention") + (("qkv_attn", "qkv_
         print(f"  entry {q(us[:, 0])}  rope {q(us[:, 2])}  attended {q(us[:, 3])}")
     else:
         print(f"  entry {q(us[:, 0])}  prologue {q(us[:, 1])}  streamed {q(us[:, 2])}  epilogue {q(us[:, 3])}")
+        if not np.all(np.isnan(us[:, 6])):
+            print(f"  A rows landed (LDS-DMA) {q(us[:, 6])}")
+
         w = us[:, 8:24]
         print(f"  waves streamed: first {q(np.nanmin(w, 1))} last {q(np.nanmax(w, 1))}  split-K barrier {q(us[:, 4])}  summed {q(us[:, 5])}")
     sys.stdout.flush()

@@ -459,6 +459,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(R * KU * NG));
       __builtin_amdgcn_s_barrier();
     }
+    TTS_STAMP(stp, 6);  // (A rows landed)
     if (a.diag & 16) {
     } else if constexpr (NORM) {
       const bf16_t* gw = (const bf16_t*)red;
