@@ -23,4 +23,6 @@ t = time.perf_counter()
 for _ in range(3):
     dec.decode_batch(utts, out=out)
 torch.cuda.synchronize()
-print(f"{B} x {T} codes: {(time.perf_counter() - t) / 3 * 1000:.2f} ms")
+import hashlib  # noqa: E402
+md5 = hashlib.md5(out.cpu().numpy().tobytes()).hexdigest()[:10]
+print(f"{B} x {T} codes: {(time.perf_counter() - t) / 3 * 1000:.2f} ms  wav md5 {md5}")
