@@ -879,6 +879,17 @@ static void launch_shape(const WgemmArgs& a, int grid, hipStream_t s) {
   // (A_GLOBAL rides A fragments in the ring: one stage deep where two would spill — KU 4, or
   // two m-tiles at KU > 2)
   const bool agr_r1 = ASRC == A_GLOBAL && (h.ku >= 4 || (a.M > 16 && h.ku > 2));
+  if constexpr (NG == 2 && ASRC == A_LDS && h.ku == 2 && h.waves == 8) {
+    // 4..16 rows, gate/up (8-wave workgroups: 256 registers a lane): a four-stage ring, so
+    // the stream keeps going through the longer LDS prologue (rows landed + RMSNorm of every
+    // row) instead of stalling once two stages have landed: TTS-1-Max 8 rows 3,380 -> 3,370 us,
+    // TTS-1 8 rows 808 -> 806 us, same ids (profiles/r4r_ab_ring4_*).  TTS_RING4=0: off
+    static const bool ring4 = !(getenv("TTS_RING4") && !atoi(getenv("TTS_RING4")));
+    if (ring4 && a.M >= 4 && a.M <= 16 && S % 4 == 0) {
+      launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 4>(a, grid, s);
+      return;
+    }
+  }
   if (h.r >= 2 && S % 2 == 0 && !agr_r1) launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 2>(a, grid, s);
   else launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 1>(a, grid, s);
 }
