@@ -96,7 +96,9 @@ typedef struct {
 } tts_lm_config;
 
 /* Loads the SpeechLM.  Weights are bf16, or f32 / f16 converted to bf16 on load (one RNE
- * rounding; lossless for f16 weights that came from the bf16 training checkpoint).  The
+ * rounding; exact for f16 values with at most 8 significant bits — the normal-range f16
+ * images of bf16 checkpoint weights — and rounding for f16 subnormals below 6.1e-5 that
+ * carry more, so such an f16 checkpoint does not load bit for bit).  The
  * engine always computes in bf16 with fp32 accumulation — the reference serving CLI's
  * fp16 arithmetic (tools/serving/inference.py:103-107) is not reproduced.
  * Optional tensors "rope.cos" / "rope.sin" ([max_seq_len, head_dim], bf16) override the

@@ -354,7 +354,8 @@ void launch_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s) {
 
 // fp16 checkpoints (the serving CLI loads the LM with torch_dtype=float16,
 // tools/serving/inference.py:103-107): f16 -> f32 is exact, then one RNE rounding to bf16
-// (exact for weights that came from the bf16 training checkpoint).
+// (exact for f16 values with at most 8 significant bits, i.e. normal-range f16 images of bf16
+// weights; f16 subnormals carrying more bits are rounded).
 __global__ void f16_to_bf16_kernel(const _Float16* __restrict__ x, bf16_t* __restrict__ y, long long n) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x)
