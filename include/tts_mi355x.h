@@ -200,8 +200,8 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
  * accounting.  which: 0 qkv projection (+RMSNorm), 1 o_proj (+residual), 2 gate/up
  * (+RMSNorm, SwiGLU), 3 down_proj (+residual), 4 lm_head (+RMSNorm, penalty, argmax
  * partials), 5 decode attention (ctx = `ctx` positions), 6 qkv with the decode attention
- * fused in (one row), 7 the same launch also carrying o_proj (+residual; the one-row
- * step's default form).  rows = batch rows.
+ * fused in (1..16 rows where that form applies), 7 the same launch also carrying o_proj
+ * (+residual; the 1..16-row step's default form where the shapes allow).  rows = batch rows.
  * Outputs: average ms per launch and the algorithmic HBM bytes one launch must move. */
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, bench, rocprofv3 kernel trace.  Every GPU step has its
 # own time limit; a crash/timeout (exit >= 124) ends the script before any further GPU work.
-# usage: scripts/gpu_round.sh TAG [tests|bench|prof]...
+# usage: scripts/gpu_round.sh TAG [tests|smoke|bench|bench32|prof]...
 set -u
 TAG=${1:-r1}; shift
 OUT=gpurun_out
@@ -11,8 +11,11 @@ stop_if_fatal() { local rc=$1; if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $2
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -rf > $OUT/${TAG}_tests.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1; rc=$?
       tail -5 $OUT/${TAG}_tests.log; stop_if_fatal $rc tests ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/${TAG}_smoke.log 2>&1; rc=$?
+      tail -3 $OUT/${TAG}_smoke.log; stop_if_fatal $rc smoke ;;
     bench)
       timeout -k 10 900 python bench.py > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err; rc=$?
       tail -3 $OUT/${TAG}_bench.err; cat $OUT/${TAG}_bench.json; stop_if_fatal $rc bench ;;

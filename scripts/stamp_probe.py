@@ -33,7 +33,7 @@ def q(v):
     return "/".join(f"{x:5.2f}" for x in (np.min(v), np.median(v), np.max(v)))
 
 
-for k in ("qkv", "o_proj", "gate_up", "down", "attention") + (("qkv_attn", "qkv_attn_oproj") if rows == 1 else ("qkv_attn",)):
+for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn_oproj"):
     for rep in range(3):
         m.bench_kernel(k, rows=rows, ctx=ctx, iters=1)
         assert f(buf.ctypes.data, N) == 0

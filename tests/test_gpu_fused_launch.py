@@ -116,16 +116,20 @@ print(hashlib.md5(out.tobytes()).hexdigest(), float(np.abs(out).max()))
 '''
 
 
-@pytest.mark.parametrize("arch,rows,L,n_last", [("tts1", 8, 1100, 24), ("tts1-max-2l", 8, 600, 24)])
+@pytest.mark.parametrize("arch,rows,L,n_last", [("tts1", 8, 1100, 24), ("tts1", 3, 700, 12),
+                                                 ("tts1-max-2l", 8, 600, 24), ("tts1-max-2l", 16, 560, 8)])
 def test_batched_fused_qkv_attention_equals_separate_launches(arch, rows, L, n_last):
     """2..16-row decode steps with the attention carried by the QKV launch (the attention
     workgroups after the projection's, one per (row, kv head), waiting on each row's tagged
-    granules) give the same bits as the separate QKV and attention launches (TTS_FATTN_ROWS=0),
-    at contexts past the attention's first pass (1,024 positions at head dim 64, 512 at 128)."""
+    granules) and o_proj behind it (its own workgroups, each wave waiting on its K range of
+    every row's attention granules) give the same bits as the QKV launch without o_proj
+    (TTS_FUSED_OPROJ_ROWS=0) and as the separate QKV, attention and o_proj launches
+    (TTS_FATTN_ROWS=0), at contexts past the attention's first pass (1,024 positions at head
+    dim 64, 512 at 128)."""
     outs = {}
-    for v in ("16", "0"):
+    for name, env in (("fused", {}), ("no_oproj", {"TTS_FUSED_OPROJ_ROWS": "0"}), ("separate", {"TTS_FATTN_ROWS": "0"})):
         r = subprocess.run([sys.executable, "-c", _ROWS_CHILD, ROOT, arch, str(rows), str(L), str(n_last)],
-                           env=dict(os.environ, TTS_FATTN_ROWS=v), capture_output=True, text=True, timeout=200)
+                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=200)
         assert r.returncode == 0, r.stderr[-2000:]
-        outs[v] = r.stdout.strip().splitlines()[-1]
-    assert outs["16"] == outs["0"], outs
+        outs[name] = r.stdout.strip().splitlines()[-1]
+    assert outs["fused"] == outs["no_oproj"] == outs["separate"], outs

@@ -238,7 +238,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.blocks.alloc(((size_t)R / 16 + B + 1) * 16);  // prefill query blocks: <= rows/16 + one per sequence
   // q|k|v granules of every decode row ([B][QKV/2]), and (one-row launches with o_proj fused)
   // the attention row's at row 1's place (a launch uses one form; every prefill resets them all)
-  w.gran.alloc(((size_t)std::max(B, 2) * QKV + H * D) / 2 * 8);
+  w.gran.alloc((size_t)std::max(B, 2) * (QKV + H * D) / 2 * 8);  // q|k|v, then attention rows
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
   {  // batched decode attention split over the context (flash-decoding chunks + merge kernel,
@@ -317,6 +317,12 @@ bool use_qkv_defer() {
 }
 bool use_kslice32() {
   static const bool v = !(getenv("TTS_KSLICE32") && !atoi(getenv("TTS_KSLICE32")));
+  return v;
+}
+// ... and at 2..16 rows, o_proj fused behind the attention of the QKV launch (its own
+// workgroups after the attention's): default on; TTS_FUSED_OPROJ_ROWS=0 keeps the launch
+bool use_fused_oproj_rows() {
+  static const bool v = !(getenv("TTS_FUSED_OPROJ_ROWS") && !atoi(getenv("TTS_FUSED_OPROJ_ROWS")));
   return v;
 }
 bool norm_in_lds32() {
@@ -498,10 +504,11 @@ struct Ctx {
     fx.fattn_spins = spins;
     if (with_oproj) {
       const LmLayer& ly = M.layers[layer];
-      const WgemmPlan po = plan_wgemm(1, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu);
+      const WgemmPlan po = plan_wgemm(a.rows, c.hidden_size, c.num_heads * c.head_dim, EPI_RESID, e->num_cu);
       fx.fo_w = ly.wo;
       fx.fo_units = c.hidden_size / 16;
       fx.fo_ur = po.sp.ur();
+      fx.fo_kc = po.sp.kc;
       fx.fo_resid = w.x.as<bf16_t>();
     }
     return fx;
@@ -520,12 +527,26 @@ struct Ctx {
            pq.sp.waves == 16 && pq.sp.ku == 2 && pq.sp.ksplit == 16;
   }
 
+  // 2..16 rows: o_proj can ride the fused QKV + attention launch when its stream plan has the
+  // launch's shape (16 waves, the QKV plan's stage width, K split 16 ways, the item = the
+  // two-stage ring) and o_proj's K is the hidden size (its A rows fit the launch's LDS rows)
+  bool fused_oproj_rows_ok(int rows) const {
+    if (!use_fused_oproj() || !use_fused_oproj_rows() || rows < 2 || rows > 16) return false;
+    const int HD = c.num_heads * c.head_dim, HID = c.hidden_size;
+    const WgemmPlan pq = plan_wgemm(rows, QKV(), HID, EPI_STORE, e->num_cu);
+    const WgemmPlan po = plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu);
+    const StreamPlan& s = po.sp;
+    return HD == HID && s.waves == 16 && s.ksplit == 16 && s.ng == 1 && s.ku == pq.sp.ku && pq.sp.waves == 16 &&
+           pq.sp.ksplit == 16 && (HD / 32) / (s.ksplit * s.ku) == 2 && (HD / 32) % (s.kc * s.ksplit * s.ku) == 0 &&
+           HID / 16 <= s.ur() && (2 * s.ku) % 4 == 0;
+  }
+
   // One transformer stack pass over `rows` rows held in w.x.
   void layers(int rows, const int* slot, const int* pos, bool decode) {
     pending_norm = nullptr;  // w.x was rewritten (embeddings) since any earlier combine
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
-    const bool foproj = fattn && rows == 1 && fused_oproj_ok();
+    const bool foproj = fattn && (rows == 1 ? fused_oproj_ok() : fused_oproj_rows_ok(rows));
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
@@ -1045,7 +1066,8 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
   TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
   TTS_REQUIRE(which < 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention does not apply to this shape");
-  TTS_REQUIRE(which != 7 || (rows == 1 && Ctx(e, e->stream).fused_oproj_ok()), "fused o_proj: one row, and on");
+  TTS_REQUIRE(which != 7 || (rows == 1 ? Ctx(e, e->stream).fused_oproj_ok() : Ctx(e, e->stream).fused_oproj_rows_ok(rows)),
+              "fused o_proj does not apply to this shape (or is off)");
   hipStream_t s = e->stream;
   Ctx X(e, s);
   const tts_lm_config& c = X.c;

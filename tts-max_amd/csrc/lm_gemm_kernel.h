@@ -117,7 +117,9 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   TTS_STAMP(stp, 2);
   dec_attend<D, PW, DEC_NW>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
                             a.out + (size_t)row * a.H * D + kvh * G * D, stp,
-                            wa.fo_units ? wa.gran + wa.N / 2 + kvh * G * D / 2 : nullptr, tag);
+                            wa.fo_units ? wa.gran + (size_t)wa.M * (wa.N / 2) + (size_t)row * (a.H * D / 2) + kvh * G * D / 2
+                                        : nullptr,
+                            tag);
   TTS_STAMP(stp, 3);
   // the new position's roped k and v to the cache, after this workgroup's reads
   if (tid < D) {
@@ -186,6 +188,87 @@ TTS_DEV void fused_oproj(const WgemmArgs& a, bf16_t* xs, float* red, int wave, i
   }
 }
 
+// The same for the 2..16-row QKV launch (FROWS, order 0): o_proj unit u on its own workgroup.
+// Each wave's K range of the o_proj plan (the launch's shape: KSPLIT == WAVES, R stages = the
+// item, fo_kc K chunks) comes from the attention rows' granules (gran + M*N/2: row m's
+// H*D/2 granules, tag = that row's (pos, layer)), R*KU/4 per lane and row, staged into the
+// wave's own columns of the LDS rows (read back by this wave only), then the o_proj launch's
+// MFMAs (rows clamped to M - 1 as its m-tile does), split-K order and residual epilogue.
+template <int KU, int KSPLIT, int R>
+TTS_DEV void fused_oproj_rows(const WgemmArgs& a, bf16_t* xs, float* red, int wave, int lane, int u) {
+  const int M = a.M, HD = a.fa.H * a.fa.D, ldxs = HD + 8, hid = a.fo_units * 16;
+  const int kpart = wave % KSPLIT;
+  const int nr = min(a.fo_ur, a.fo_units);
+  const int KTc = (HD >> 5) / a.fo_kc, kt_pc = KTc / KSPLIT, Sc = kt_pc / KU;
+  auto ktile = [&](int st, int kk) {  // absolute k-tile of stage st, tile kk of this wave
+    const int ch = st / Sc;
+    return ch * KTc + kpart * kt_pc + (st - ch * Sc) * KU + kk;
+  };
+  u32x4_t wr[R][KU];
+#pragma unroll
+  for (int st = 0; st < R; ++st)
+#pragma unroll
+    for (int kk = 0; kk < KU; ++kk)
+      wr[st][kk] = __builtin_nontemporal_load((const u32x4_t*)a.fo_w +
+                                              ((((long long)st * nr + u) * KSPLIT + kpart) * KU + kk) * 64 + lane);
+  bf16_t rr[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rr[r] = a.fo_resid[(size_t)min(4 * (lane >> 4) + r, M - 1) * hid + u * 16 + (lane & 15)];
+  constexpr int NGL = R * KU >= 4 ? R * KU / 4 : 1;  // granules per lane and row (R*KU k-tiles of 16; host: R*KU % 4 == 0)
+  int col[NGL];
+#pragma unroll
+  for (int j = 0; j < NGL; ++j) {
+    const int gi = j * 64 + lane, ktl = gi >> 4;
+    col[j] = ktile(ktl / KU, ktl % KU) * 32 + (gi & 15) * 2;
+  }
+  const uint64_t* g0 = a.gran + (size_t)M * (a.N / 2);
+  for (int m = 0; m < M; ++m) {
+    const uint32_t tag = ((uint32_t)a.fa.row_pos[m] << 6) | (uint32_t)a.fattn_layer;
+    uint64_t v[NGL];
+    fattn_wait([&] {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < NGL; ++j) {
+        v[j] = __hip_atomic_load(g0 + (size_t)m * (HD / 2) + col[j] / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && (uint32_t)(v[j] >> 32) == tag;
+      }
+      return (bool)__all(ok);
+    }, a.fattn_err, a.fattn_spins, lane == 0);
+#pragma unroll
+    for (int j = 0; j < NGL; ++j) *(uint32_t*)(xs + (size_t)m * ldxs + col[j]) = (uint32_t)v[j];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* xr = xs + (size_t)min(lane & 15, M - 1) * ldxs + 8 * (lane >> 4);
+#pragma unroll
+  for (int st = 0; st < R; ++st)
+#pragma unroll
+    for (int kk = 0; kk < KU; ++kk) {
+      const u32x4_t av = *(const u32x4_t*)(xr + ktile(st, kk) * 32);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av), as_bf16x8(wr[st][kk]), acc, 0, 0, 0);
+    }
+  if (kpart > 0) *(f32x4_t*)(red + ((size_t)(kpart - 1) * 64 + lane) * 4) = acc;
+  lds_barrier();
+  if (kpart == 0) {
+    constexpr int HB = 8;
+#pragma unroll
+    for (int p0 = 1; p0 < KSPLIT; p0 += HB) {
+      f32x4_t pv[HB];
+#pragma unroll
+      for (int j = 0; j < HB; ++j)
+        if (p0 + j < KSPLIT) pv[j] = *(const f32x4_t*)(red + ((size_t)(p0 + j - 1) * 64 + lane) * 4);
+#pragma unroll
+      for (int j = 0; j < HB; ++j)
+        if (p0 + j < KSPLIT) acc += pv[j];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 4 * (lane >> 4) + r;
+      if (m < M) a.fo_resid[(size_t)m * hid + u * 16 + (lane & 15)] = f2bf(bf2f(rr[r]) + rbf(acc[r]));
+    }
+  }
+}
+
 // ---------------------------------------------------------------- the GEMM kernel -----
 // One workgroup = WAVES waves; KSPLIT consecutive waves split the K range of one unit
 // (a unit = NG n-tiles of 16 output columns), WAVES/KSPLIT units run side by side, and
@@ -229,9 +312,13 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       if (cb >= a.fattn_wgs) {  // (order 0) o_proj unit cb - fattn_wgs
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const uint32_t tag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
         const size_t xs_bytes = (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15);
-        fused_oproj<KU, KSPLIT, R>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane, tag, cb - a.fattn_wgs);
+        if constexpr (FROWS) {
+          fused_oproj_rows<KU, KSPLIT, R>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane, cb - a.fattn_wgs);
+        } else {
+          const uint32_t tag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
+          fused_oproj<KU, KSPLIT, R>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane, tag, cb - a.fattn_wgs);
+        }
         return;
       }
     }
@@ -816,9 +903,15 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
       throw std::runtime_error("wgemm: fused attention needs a 1..16-row 16-wave QKV launch (D 64 or 128)");
     if ((a.M == 1) != EARLY)
       throw std::runtime_error("wgemm: fused attention: one row = the register-staged prologue, 2..16 rows = not");
-    if (a.M > 1 && (a.fattn_first || a.fo_units))
-      throw std::runtime_error("wgemm: multi-row fused attention: producer-first grid order, no fused o_proj");
-    if (a.fo_units) {  // fused o_proj: one unit per o_proj (order 1: projection) workgroup, one granule per lane
+    if (a.M > 1 && a.fattn_first)
+      throw std::runtime_error("wgemm: multi-row fused attention: producer-first grid order only");
+    if (a.fo_units && a.M > 1) {  // fused o_proj behind the 2..16-row attention (order 0)
+      const int HD = a.fa.H * a.fa.D;
+      const int S = (HD / 32) / (KSPLIT * KU);
+      if (!(a.fo_w && a.fo_resid && a.fo_units <= a.fo_ur && S == R && KSPLIT == WAVES && HD == a.K && a.fo_kc >= 1 &&
+            (HD / 32) % (a.fo_kc * KSPLIT * KU) == 0 && R * KU % 4 == 0 && R * KU >= 4))
+        throw std::runtime_error("wgemm: fused multi-row o_proj shape mismatch");
+    } else if (a.fo_units) {  // fused o_proj: one unit per o_proj (order 1: projection) workgroup, one granule per lane
       const int S = (a.fa.H * a.fa.D / 32) / (KSPLIT * KU);
       if (!(a.fo_w && a.fo_resid && (!a.fattn_first || a.fo_units <= grid) && a.fo_units <= a.fo_ur && S == R &&
             a.fa.H * a.fa.D == KSPLIT * 128 && KSPLIT == WAVES && (size_t)a.M * (a.K + 8) * 2 >= (size_t)KSPLIT * 256))

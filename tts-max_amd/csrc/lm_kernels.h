@@ -122,7 +122,7 @@ struct WgemmArgs {
   // head, load their K / V^T fragments, wait for their q (and the new k/v) granules and
   // attend exactly as attn_decode_kernel does.  tag = (pos << 6) | layer differs between any
   // two consecutive launches, so a granule left by the previous launch never matches.
-  uint64_t* gran = nullptr;   // [M][ldo / 2]
+  uint64_t* gran = nullptr;   // [M][N / 2] q|k|v granules, then (fo_units) [M][H*D / 2] attention rows
   AttnArgs fa;                // the attention of this layer (its output row: fa.out)
   int fattn_wgs = 0;          // attention workgroups appended to the grid (0: not fused)
   int fattn_layer = 0;
@@ -140,8 +140,10 @@ struct WgemmArgs {
   // fo_w, layout rounds fo_ur, one round) runs on the grid's b-th o_proj workgroup (order 0)
   // or on projection workgroup b after its QKV unit (order 1), with the residual epilogue on
   // fo_resid (the hidden row), its o_proj weights loaded while the attention runs
+  // (2..16 rows, order 0: the attention rows' granules at gran + M*N/2, row m's H*D/2 at
+  // m*H*D/2; o_proj's layout K chunks fo_kc; fo_resid holds the M hidden rows)
   const bf16_t* fo_w = nullptr;
-  int fo_units = 0, fo_ur = 0;
+  int fo_units = 0, fo_ur = 0, fo_kc = 1;
   bf16_t* fo_resid = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS): [block][8]
   int csplit = 1;     // 2: each 16-column unit runs as two 8-column halves (twice the workgroups; filled in by launch_wgemm)
