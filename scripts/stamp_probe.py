@@ -51,9 +51,14 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn
         # grid order (WgemmArgs::fattn_first): default projection | attention | o_proj workgroups;
         # TTS_FATTN_FIRST=1: attention first
         first = os.environ.get("TTS_FATTN_FIRST", "0") == "1"
-        nq = len(us) - rows * arch.num_kv_heads  # projection workgroups (the o_proj ones write no stamps)
         na = rows * arch.num_kv_heads
+        # (the one-row o_proj workgroups write no stamps; the 2..16-row ones do, last in the grid)
+        no = arch.hidden_size // 16 if (k == "qkv_attn_oproj" and rows > 1) else 0
+        nq = len(us) - na - no  # projection workgroups
         proj, cons = (us[na:], us[:na]) if first else (us[:nq], us[nq:nq + na])
+        if no:
+            op = us[nq + na:]
+            print(f"  o_proj      entry {q(op[:, 0])}  row 0 granules {q(op[:, 1])}  all rows {q(op[:, 2])}  done {q(op[:, 3])}")
 
         print(f"  projection  entry {q(proj[:, 0])}  prologue {q(proj[:, 1])}  streamed {q(proj[:, 2])}  epilogue {q(proj[:, 3])}")
         print(f"  attention   entry {q(cons[:, 0])}  granules {q(cons[:, 1])}  rope {q(cons[:, 2])}  max {q(cons[:, 5])}  pv {q(cons[:, 6])}  attended {q(cons[:, 3])}")
