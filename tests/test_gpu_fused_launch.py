@@ -116,8 +116,9 @@ print(hashlib.md5(out.tobytes()).hexdigest(), float(np.abs(out).max()))
 '''
 
 
-@pytest.mark.parametrize("arch,rows,L,n_last", [("tts1", 8, 1100, 24), ("tts1", 3, 700, 12),
-                                                 ("tts1-max-2l", 8, 600, 24), ("tts1-max-2l", 16, 560, 8)])
+@pytest.mark.parametrize("arch,rows,L,n_last", [("tts1", 8, 1100, 24), ("tts1", 3, 700, 12), ("tts1", 2, 400, 12),
+                                                 ("tts1", 16, 500, 8), ("tts1-max-2l", 8, 600, 24),
+                                                 ("tts1-max-2l", 16, 560, 8)])
 def test_batched_fused_qkv_attention_equals_separate_launches(arch, rows, L, n_last):
     """2..16-row decode steps with the attention carried by the QKV launch (the attention
     workgroups after the projection's, one per (row, kv head), waiting on each row's tagged
