@@ -1,4 +1,4 @@
-"""The one-row decode step's fused QKV + attention + o_proj launch (lm_gemm_kernel.h) under
+"""The decode step's fused QKV + attention + o_proj launches (lm_gemm_kernel.h) under
 adverse conditions:
 
 * its grid order (projection workgroups, then attention, then o_proj workgroups) lets every
@@ -26,18 +26,24 @@ def _tts1_prompt():
     return synth.synthetic_prompt(configs.vocab_for(configs.TTS1), 5, 39, 150)
 
 
-def test_b1_generation_beside_concurrent_encodes():
+@pytest.mark.parametrize("arch_name,rows", [("tts1", 1), ("tts1", 8), ("tts1-max-2l", 8)])
+def test_generation_beside_concurrent_encodes(arch_name, rows):
+    """One row (QKV + attention + o_proj in one launch) and 8 rows (the 2..16-row form: the
+    attention workgroups, then one o_proj workgroup per unit spinning on the attention's
+    granules) complete beside a loop of prompt encodes on another stream, with the ids they
+    give alone and no granule-wait timeout."""
     import torch
 
     from tts_amd import configs, synth
     from tts_amd.encoder import MI355XAudioEncoder
     from tts_amd.speechlm import MI355XSpeechLM
 
-    arch = configs.TTS1
-    p = _tts1_prompt()
-    m = MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=1, max_seq_len=len(p) + 320)
-    kw = dict(max_length=len(p) + 300, min_new_tokens=300, eos_token_id=-1, repetition_penalty=1.1)
-    alone = m.generate_batch([p], **kw)[0]
+    arch = configs.LM_ARCHS[arch_name]
+    p = synth.synthetic_prompt(configs.vocab_for(arch), 5, 39, 150)
+    n = 300 if rows == 1 else 120
+    m = MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=rows, max_seq_len=len(p) + n + 20)
+    kw = dict(max_length=len(p) + n, min_new_tokens=n, eos_token_id=-1, repetition_penalty=1.1)
+    alone = m.generate_batch([p] * rows, **kw)
     enc = MI355XAudioEncoder.synthetic(device=0)
     wav = torch.from_numpy(synth.synthetic_wav(3, 48000))[None]
     feats = enc.features(wav)
@@ -56,7 +62,7 @@ def test_b1_generation_beside_concurrent_encodes():
     t = threading.Thread(target=encoder_loop)
     t.start()
     try:
-        together = [m.generate_batch([p], **kw)[0] for _ in range(3)]
+        together = [m.generate_batch([p] * rows, **kw) for _ in range(3)]
     finally:
         stop.set()
         t.join()
@@ -134,3 +140,18 @@ def test_batched_fused_qkv_attention_equals_separate_launches(arch, rows, L, n_l
         assert r.returncode == 0, r.stderr[-2000:]
         outs[name] = r.stdout.strip().splitlines()[-1]
     assert outs["fused"] == outs["no_oproj"] == outs["separate"], outs
+
+
+@pytest.mark.parametrize("env", [{"TTS_FATTN_FIRST": "1"}, {"TTS_FATTN_FIRST": "1", "TTS_FUSED_OPROJ": "0"},
+                                 {"TTS_FUSED_OPROJ": "0"}, {"TTS_FUSED_ATTN": "0"}])
+def test_one_row_grid_orders_equal(env):
+    """The one-row fused launch in round 3's grid order (TTS_FATTN_FIRST=1: attention
+    workgroups first, o_proj on the projection workgroups after their QKV unit), with and
+    without o_proj fused, gives the default launch's bits (and the separate launches')."""
+    outs = []
+    for e in ({}, env):
+        r = subprocess.run([sys.executable, "-c", _ROWS_CHILD, ROOT, "tts1", "1", "1100", "24"],
+                           env=dict(os.environ, **e), capture_output=True, text=True, timeout=200)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1], outs

@@ -21,6 +21,16 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 #define TTS_STAMP(buf, slot) do {} while (0)
 #define TTS_STAMP_WAVE(buf, slot) do {} while (0)
 #endif
+// Timing-diagnostic switches of the GEMM kernel (WgemmArgs::diag, TTS_WGEMM_DIAG) exist in the
+// diagnostic build only.  In the product build they must not exist even as untaken branches:
+// a branch that skips the LDS-DMA landing wait leaves the DMA "pending" on one path, and the
+// compiler's wait insertion merges paths pessimistically, i.e. puts s_waitcnt vmcnt(0) (drain
+// the whole weight ring) before the first LDS read of the prologue.
+#ifdef TTS_STAMPS
+constexpr int kWgemmDiagMask = ~0;
+#else
+constexpr int kWgemmDiagMask = 0;
+#endif
 
 // bf16 -> fp32 is exact: the bf16 bits are the top half of the fp32 pattern.
 // Workgroup barrier ordering LDS only: unlike __syncthreads (which waits for every

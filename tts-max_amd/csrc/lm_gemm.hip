@@ -135,6 +135,10 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   p.grid = p.sp.grid;
   const int w = p.sp.waves, ks = p.sp.ksplit;
   p.a_lds = wgemm_lds_bytes(w, ks, ng, M, K, true) <= kLdsBudget;
+  // the LDS prologues stage rows in 512-column pieces (LDS-DMA) or registers (also K % 512 ==
+  // 0); other widths (small test configs) take A fragments from global memory + a standalone
+  // RMSNorm (same canonical sum order: same bits)
+  if (K % 512 != 0) p.a_lds = false;
   // experiment hook: TTS_HEAD_GRID=<workgroups> for the lm_head launch (units are walked
   // grid-stride, so any grid covers them; at most LOGITS_MAX_PARTS argmax partials)
   static const int head_grid = getenv("TTS_HEAD_GRID") ? atoi(getenv("TTS_HEAD_GRID")) : 0;
@@ -204,7 +208,11 @@ bool wgemm_fattn_ok(int N, int K, int num_cu) {
 // 16-wave, unsliced launch with the A rows in LDS (any prologue)
 bool wgemm_fattn_rows_ok(int M, int N, int K, int D, int num_cu) {
   const WgemmPlan p = plan_wgemm(M, N, K, EPI_STORE, num_cu);
-  return M >= 2 && M <= 16 && p.a_lds && !p.sliced && p.sp.waves == DEC_NW && D == wgemm_fattn_d(p.sp.ku);
+  // (launch_wgemm runs the fused launch with whole units, csplit 1; the launch shape's ring
+  // depth is 2 when the item's stage count is even, which the fused o_proj also requires)
+  const int S = (K / 32) / (p.sp.ksplit * p.sp.ku);
+  return M >= 2 && M <= 16 && p.a_lds && !p.sliced && p.sp.waves == DEC_NW && D == wgemm_fattn_d(p.sp.ku) &&
+         K % 512 == 0 && S % 2 == 0;
 }
 
 bool wgemm_supported(int M, int N, int K, int epi) {

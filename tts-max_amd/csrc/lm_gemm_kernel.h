@@ -327,7 +327,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         fattn_consumer<NT, wgemm_fattn_d(KU)>(a, smem, cb);
         return;
       }
-      if (cb >= a.fattn_wgs) {  // (order 0) o_proj unit cb - fattn_wgs
+      if (!a.fattn_first && cb >= a.fattn_wgs) {  // (order 0) o_proj unit cb - fattn_wgs
         const int lane = threadIdx.x & 63;
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const size_t xs_bytes = (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15);
@@ -394,6 +394,16 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // before the whole first weight stage had landed.
   const int tid = threadIdx.x;
   const int kch = a.K >> 3;  // 16-B chunks per A row
+  // (2..16-row fused attention) the granule tags of the rows: each lane of wave 0 loads one
+  // row's position here, ahead of every other load, and parks the tag in LDS after the
+  // prologue's landing wait (the epilogue reads it there).  Computed from the load on the spot,
+  // the tags would need a vmcnt(0) before the weight stream is even issued (the A rows' DMA is
+  // still in flight), and held in registers through the stream they spilled.
+  constexpr bool FTAGS = FATT && !EARLY;
+  int ftag_pos = 0;
+  if constexpr (FTAGS) {
+    if (a.fattn_wgs) ftag_pos = a.fa.row_pos[min(lane & 15, M - 1)];
+  }
   // (a) A rows (+ RMSNorm weight) for the LDS prologue, EA chunks per thread at most
   constexpr int EA = wgemm_ea(WAVES);
   const int achunks = M * kch;
@@ -415,8 +425,12 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   //      instruction, one row piece each) straight into the padded LDS rows, and the RMSNorm
   //      weight into the (still unused) split-K scratch — no VGPRs, and issued ahead of the
   //      weight stream like every other operand
+  // (the only LDS prologue besides the early one: the host sends rows whose K is not a
+  // multiple of 512 through A_GLOBAL + a standalone RMSNorm instead (plan_wgemm).  A second,
+  // runtime-selected prologue form would leave its loads "pending" at the join for the
+  // compiler's wait insertion, i.e. a vmcnt(0) that drains the weight ring before the stream.)
   constexpr bool glds_ok = ASRC == A_LDS && !early_a;
-  const bool use_glds = glds_ok && (a.K & 511) == 0;
+  constexpr bool use_glds = glds_ok;
   if constexpr (glds_ok) {
     if (use_glds) {
       const int ppr = a.K >> 9;
@@ -452,16 +466,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
 
   uint32_t ftag = 0;  // fused attention: this launch's granule tag (row 0)
-  uint32_t ftagr[4] = {0u, 0u, 0u, 0u};  // (2..16 rows) the tags of this lane's accumulator rows
-  if constexpr (FATT) {
-    if (a.fattn_wgs) {
-      ftag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
-      if constexpr (!EARLY) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          ftagr[r] = ((uint32_t)a.fa.row_pos[min(4 * (lane >> 4) + r, M - 1)] << 6) | (uint32_t)a.fattn_layer;
-      }
-    }
+  if constexpr (FATT && EARLY) {
+    if (a.fattn_wgs) ftag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
   }
 
   // ---- then the weight stream
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // scheduling barrier stops the compiler sinking an operand load below the weight stream
   // (each prologue wait would then drain the primed stages too)
   __builtin_amdgcn_sched_barrier(0);
-  if (a.diag & 8) __syncthreads();
+  if (a.diag & kWgemmDiagMask & 8) __syncthreads();
   // (unconditional: a wave with no unit streams unit units-1, never consumed (sptr clamps).
   // A branch here would make every prologue wait below drain the primed stages as well)
 #pragma unroll
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- prologue: A rows in LDS (plain, RMSNorm'ed, or combined from attention chunks)
-  if (a.diag & 1) {
+  if (a.diag & kWgemmDiagMask & 1) {
   } else if constexpr (ASRC == A_LDS) {
    if constexpr (early_a) {
     // rows already in registers: RMSNorm statistics per 64-chunk wave segment (DPP), the
@@ -557,15 +563,15 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
     lds_barrier();
-   } else if (use_glds) {
+   } else if constexpr (use_glds) {
     // rows landed by LDS-DMA: wait for this wave's DMA only (the weight ring issued after
     // it stays in flight), then every wave's (raw barrier: __syncthreads would drain the ring)
-    if (!(a.diag & 32)) {
+    if (!(a.diag & kWgemmDiagMask & 32)) {
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(R * KU * NG));
       __builtin_amdgcn_s_barrier();
     }
     TTS_STAMP(stp, 6);  // (A rows landed)
-    if (a.diag & 16) {
+    if (a.diag & kWgemmDiagMask & 16) {
     } else if constexpr (NORM) {
       const bf16_t* gw = (const bf16_t*)red;
       for (int m = wave; m < M; m += WAVES) {
@@ -586,65 +592,15 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
       __builtin_amdgcn_s_barrier();
     }
-   } else {
-    // general rows (more than the early registers hold): 16-B copies into LDS, 4 per
-    // thread in flight (clamped, unconditional loads), then RMSNorm in place, a wave per row.
-    // The lane's RMSNorm weight chunks (k = lane*8 + 512 i) ride with the first copy batch:
-    // loaded inside the per-row loop they would be a chain of dependent L2 round trips.
-    constexpr int NKX = 8;  // K <= 4096 (host: fused RMSNorm only up to K = 4096)
-    u32x4_t gw[NORM ? NKX : 1];
-    for (int c0 = 0; c0 < achunks; c0 += 4 * NT) {
-      u32x4_t v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = min(c0 + tid + j * NT, achunks - 1);
-        const int m = c / kch, k = (c - m * kch) * 8;
-        v[j] = *(const u32x4_t*)(xg + (size_t)m * a.ldx + k);
-      }
-      if constexpr (NORM) {
-        if (c0 == 0) {
-#pragma unroll
-          for (int i = 0; i < NKX; ++i) gw[i] = *(const u32x4_t*)(a.normw + min(lane * 8 + i * 512, a.K - 8));
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = c0 + tid + j * NT;
-        if (c < achunks) {
-          const int m = c / kch, k = (c - m * kch) * 8;
-          *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v[j];
-        }
-      }
-    }
-    if constexpr (NORM) {
-      lds_barrier();
-      for (int m = wave; m < M; m += WAVES) {
-        bf16_t* xr = xs + (size_t)m * ldxs;
-        float ss = 0.f;
-        for (int k0 = 0; k0 < a.K; k0 += 512) {  // canonical order (chunk_sumsq)
-          const int k = k0 + lane * 8;
-          const float s = k < a.K ? chunk_sumsq(*(const u32x4_t*)(xr + k)) : 0.f;
-          ss += wave_sum_dpp(s);
-        }
-        const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-#pragma unroll
-        for (int i = 0; i < NKX; ++i) {
-          const int k = lane * 8 + i * 512;
-          if (k < a.K) {
-            u32x4_t v = *(const u32x4_t*)(xr + k);
-            const u32x4_t g = gw[i];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
-            *(u32x4_t*)(xr + k) = v;
-          }
-        }
-      }
-    }
-    lds_barrier();
    }
   }
   TTS_STAMP(stp, 1);
+  // (the tags' LDS slots: the last 16 floats of the scratch region's slack; read after the
+  // split-K combine's barriers)
+  uint32_t* ftag_lds = (uint32_t*)(red + wgemm_red_floats(WAVES, KSPLIT, NG, MT_MAX, M, a.K) - 16);
+  if constexpr (FTAGS) {
+    if (a.fattn_wgs && wave == 0 && lane < 16) ftag_lds[lane] = ((uint32_t)ftag_pos << 6) | (uint32_t)a.fattn_layer;
+  }
 
   // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
   float best_v[MT_MAX][4];
@@ -716,7 +672,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     }
 
     if (first) { TTS_STAMP(stp, 2); TTS_STAMP_WAVE(stp, 8 + wave); }
-    if (a.diag & 2) {
+    if (a.diag & kWgemmDiagMask & 2) {
       if (acc[0][0][0] == 1234.5f && a.out) a.out[0] = 0;
       continue;
     }
@@ -794,11 +750,12 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int m = mt * 16 + 4 * (lane >> 4) + r;
           if (m >= M) continue;
+          // (32-bit element offsets: 64-bit ones hoisted out of the unit loop cost registers)
           if constexpr (EPI == EPI_STORE) {
-            if (a.part_out) a.part_out[((size_t)blockIdx.y * M + m) * a.ldo + n] = acc[0][mt][r];
-            else a.out[(size_t)m * a.ldo + n] = f2bf(acc[0][mt][r]);
+            if (a.part_out) a.part_out[((int)blockIdx.y * M + m) * a.ldo + n] = acc[0][mt][r];
+            else a.out[m * a.ldo + n] = f2bf(acc[0][mt][r]);
           } else if constexpr (EPI == EPI_RESID) {
-            bf16_t* p = a.resid + (size_t)m * a.ldo + n;
+            bf16_t* p = a.resid + (m * a.ldo + n);
             *p = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
           } else if constexpr (EPI == EPI_SWIGLU) {
             // unit u = (gate tile, up tile) pair for intermediate columns u*16 .. u*16+15
@@ -835,8 +792,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             const int m = 4 * (lane >> 4) + r;
             if (!(lane & 1) && m < M) {
               const int n = u * 16 + (lane & 15);
-              const uint64_t g = ((uint64_t)ftagr[r] << 32) | (other << 16) | mine;
-              __hip_atomic_store(a.gran + (size_t)m * (a.N / 2) + n / 2, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const uint64_t g = ((uint64_t)ftag_lds[m] << 32) | (other << 16) | mine;
+              __hip_atomic_store(a.gran + (m * (a.N >> 1) + (n >> 1)), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
         }
@@ -953,6 +910,8 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
     }
   }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
+  if (ASRC == A_LDS && !EARLY && a.K % 512 != 0)
+    throw std::runtime_error("wgemm: the LDS-DMA prologue needs K a multiple of 512 (plan_wgemm: A_GLOBAL)");
   const dim3 g(grid, a.sliced ? a.kc : 1);
   if (mt == 1 && !EARLY && a.fattn_wgs && a.M > 1) {
     if constexpr (EPI == EPI_STORE && ASRC == A_LDS && WAVES == DEC_NW)
