@@ -277,7 +277,8 @@ def main():
                            x_realtime=round(32 * N / carch.token_rate / e32, 2), lm_prefill_ms=round(a32, 3),
                            lm_decode_ms=round(b32, 3), decode_step_ms=round(b32 / max(k32, 1), 4),
                            codec_ms=round(codec32_ms, 3), codec_utterances=32, codec_codes_per_utterance=codes_per_utt,
-                           codec_roofline=codec_roofline(carch, codes_per_utt, 32, codec32_ms))
+                           codec_roofline=codec_roofline(carch, codes_per_utt, 32, codec32_ms),
+                           prefill_roofline=prefill_roofline(arch, [len(q) for q in p32], a32))
         # the 32-row decode kernels: live HIP-event time, algorithmic bytes, PMC HBM traffic
         k32s = {}
         for k in lm.KERNELS:
@@ -351,6 +352,8 @@ def main():
             "codec_ms": round(codec_ms, 3),
             "codec_to_host_ms": round(codec_host_ms, 3),
             "codec_roofline": codec_roofline(carch, codes_per_utt, B, codec_ms),
+            "prefill_roofline": prefill_roofline(arch, [len(q) for q in prompts_all[rank * B:(rank + 1) * B]],
+                                                 lm_prefill / args.steps),
             "config": {
                 "workload": f"{arch.name} bf16 bs={B}/GPU: prompt {P} tokens ({args.prompt_codes} codes), "
                             f"{N} greedy codes, codec {carch.name} on {codes_per_utt} codes",
@@ -402,6 +405,27 @@ def codec_roofline(carch, T, n_utt, ms):
     return dict(bound="mfma", achieved=round(ach, 1), peak=round(peak, 1), unit="TFLOP/s (fp32-equivalent)",
                 frac=round(ach / peak, 4), flops=fl, ms=round(ms, 3), utterances=n_utt, codes_per_utterance=T,
                 note="split-bf16 GEMMs: 6 bf16 MFMA products per fp32 multiply-add; peak = 2.5 PF / 6")
+
+
+def prefill_flops(arch, lens):
+    """SURVEY 8(d) prefill FLOPs of a batch of prompts: 2 * (layer weights) * P per prompt +
+    causal attention 2 * 2 * P^2 / 2 * (H * D) per layer + the lm_head on each prompt's last
+    token (inferencing.py:94-107, the first generate iteration)."""
+    H, KVH, D, HID, FF = arch.num_heads, arch.num_kv_heads, arch.head_dim, arch.hidden_size, arch.intermediate_size
+    w_layers = arch.num_layers * (HID * (H + 2 * KVH) * D + H * D * HID + 3 * HID * FF + 2 * HID)
+    f = 0.0
+    for P in lens:
+        f += 2.0 * w_layers * P + arch.num_layers * 2.0 * P * P * H * D + 2.0 * arch.vocab_size * HID
+    return f
+
+
+def prefill_roofline(arch, lens, ms):
+    """MFMA roofline of the prefill (prefill GEMMs + causal attention + the first lm_head):
+    bf16 FLOP/s against the dense bf16 MFMA peak."""
+    fl = prefill_flops(arch, lens)
+    ach = fl / (ms * 1e-3) / 1e12
+    return dict(bound="mfma", achieved=round(ach, 1), peak=BF16_MFMA_PEAK_TFLOPS, unit="TFLOP/s", frac=round(
+        ach / BF16_MFMA_PEAK_TFLOPS, 4), flops=fl, ms=round(ms, 3), prompts=len(lens), prompt_tokens=sum(lens))
 
 
 def synthetic_codes(lm, ids):
@@ -500,6 +524,13 @@ def cpu_baseline(arch, carch, prompt, N, args):
         legs[threads] = (n, t_p, t_d)
         log(f"cpu baseline: {threads} threads: {n} codes, {t_d * 1000:.1f} ms/code")
     best = min(legs, key=lambda t: legs[t][1] + (N - 1) * legs[t][2])
+    # HF generate in fp32 as well as bf16 (the reference CLI loads bf16 or fp16;
+    # fp32 is the CPU's native arithmetic): a shorter bounded sample at the winning thread count
+    model = model.float()
+    S32 = max(8, args.cpu_steps // 3)
+    log(f"cpu baseline: fp32, {best} threads, prefill + up to {S32} codes (30 s budget) ...")
+    t_p32, t_d32, n32 = lm_leg(best, S32, 30.0)
+    log(f"cpu baseline: fp32: {n32} codes, {t_d32 * 1000:.1f} ms/code")
     del model
     torch.set_num_threads(best)
     cw = synth.codec_weights_cpu(carch, 0xC0DEC)
@@ -521,10 +552,16 @@ def cpu_baseline(arch, carch, prompt, N, args):
         "by_threads": {str(t): {"codes_per_s": round(N / (v[1] + (N - 1) * v[2] + t_codec), 3),
                                 "prefill_s": round(v[1], 3), "ms_per_code": round(1000 * v[2], 2),
                                 "sample_codes": v[0]} for t, v in legs.items()},
+        "by_dtype": {"bf16": {"codes_per_s": round(N / full, 3), "prefill_s": round(t_prefill, 3),
+                              "ms_per_code": round(1000 * t_dec, 2), "sample_codes": S, "threads": best},
+                     "fp32": {"codes_per_s": round(N / (t_p32 + (N - 1) * t_d32 + t_codec), 3),
+                              "prefill_s": round(t_p32, 3), "ms_per_code": round(1000 * t_d32, 2),
+                              "sample_codes": n32, "threads": best}},
         "sample": (f"transformers {__import__('transformers').__version__} LlamaForCausalLM.generate (bf16, greedy, "
                    f"rep 1.1; the reference's LM call) on the same weights at {best} threads: prefill {len(prompt)} "
                    f"tokens ({t_prefill:.2f}s) + {S} generated codes ({t_dec * 1000:.1f} ms/code), extrapolated to "
-                   f"{N} codes; codec as the fp32 port on the whole {T_s}-code utterance ({t_codec:.2f}s)"),
+                   f"{N} codes; codec as the fp32 port on the whole {T_s}-code utterance ({t_codec:.2f}s); "
+                   f"value = the bf16 leg, by_dtype adds the same job in fp32 ({n32} codes sampled)"),
     }
 
 
