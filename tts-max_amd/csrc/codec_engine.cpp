@@ -56,7 +56,10 @@ struct Codec {
   DevBuf b0, b1, b2, big, qkv, stats, head, spec, frames;
   DevBuf meta;   // segment tables, wave offsets, code rows, attention query blocks
   DevBuf planes;  // every GEMM weight (B operand) split once into its bf16 h / m / l planes
-  DevBuf aplanes;  // TTS_CODEC_APRE: the current GEMM's A operand split into planes
+  // bf16 planes [3][rows * C] of the activations only GEMMs read (gemm_x3p's A operand, the
+  // same element offsets as the fp32 buffer they replace): b2 (RMSNorm / attention / GroupNorm +
+  // swish outputs) and the fc1 -> fc2 hidden (4 D wide)
+  DevBuf b2p, bigpp;
   DevBuf rope_cs;  // [heads][32][cos, sin] of the attention's RoPE
   std::map<const float*, const uint16_t*> bplanes;
   DevBuf codes, wav;  // all utterances' codes; host-bound waveforms staged on the device
@@ -313,17 +316,30 @@ void gemm(const float* A, int M, int K, int lda, const float* B, int N, const fl
   auto it = t_codec->bplanes.find(B);
   if (it != t_codec->bplanes.end()) g.Bp = it->second;
   g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
-  // experiment hook TTS_CODEC_APRE=1: A split into its bf16 planes by one pass, shared by every
-  // N tile of the big GEMMs (instead of each workgroup splitting its A tiles while staging)
-  static const bool apre = getenv("TTS_CODEC_APRE") && atoi(getenv("TTS_CODEC_APRE"));
-  if (apre && g.Bp && M >= 4096 && K % 32 == 0 && lda % 8 == 0) {
-    const long long span = (long long)(M - 1) * lda + K;
-    if (t_codec->aplanes.bytes < (size_t)span * 6) t_codec->aplanes.alloc((size_t)span * 6);
-    launch_split_planes(A, t_codec->aplanes.as<uint16_t>(), span, s);
-    g.Ap = t_codec->aplanes.as<uint16_t>();
-    g.ap_plane = span;
-  }
   launch_gemm_f32(g, s);
+}
+
+// The same GEMM with A given as bf16 planes written by its producer (Ap: the planes image of
+// A's first element, plane stride ap_plane) and optionally the output as planes too (Cp):
+// gemm_x3p, no split in the GEMM (codec_gemm.hip)
+void gemm_p(const uint16_t* Ap, long long ap_plane, int M, int K, int lda, const float* B, int N, const float* bias,
+            float* C, int ldc, const float* resid, int act, hipStream_t s, uint16_t* Cp = nullptr,
+            long long cp_plane = 0) {
+  GemmF32Args g;
+  g.Ap = Ap; g.ap_plane = ap_plane;
+  g.M = M; g.K = K; g.lda = lda; g.B = B; g.N = N; g.bias = bias;
+  auto it = t_codec->bplanes.find(B);
+  TTS_REQUIRE(it != t_codec->bplanes.end(), "codec: weight planes missing");
+  g.Bp = it->second;
+  g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
+  g.Cp = Cp; g.cp_plane = cp_plane;
+  launch_gemm_x3p(g, s);
+}
+
+// TTS_CODEC_X3P=0: the fp32-staging GEMM (gemm_bx3_kernel splits A while staging) everywhere
+bool use_x3p() {
+  static const bool v = !(getenv("TTS_CODEC_X3P") && !atoi(getenv("TTS_CODEC_X3P")));
+  return v;
 }
 
 // The utterances of one pass at one time resolution: segment table (device), padded rows.
@@ -337,18 +353,24 @@ struct Level {
 // ResnetBlock (decoder_modules.py:162-223) on ragged time-major buffers: x -> out, tmp is
 // scratch (its gap rows are the convs' zero padding, written by groupnorm_swish).
 void resnet(const CodecResBlock& rb, float* x, float* tmp, float* out, const Level& lv, int B,
-            float* stats, hipStream_t s) {
+            float* stats, hipStream_t s, uint16_t* tmpp = nullptr, long long tplane = 0) {
   const int C = rb.C;
   float* xr = x + (size_t)kPad * C;
   float* tr = tmp + (size_t)kPad * C;
   float* orow = out + (size_t)kPad * C;
+  // (tmpp: GroupNorm + swish write tmp's planes, the convs read them with gemm_x3p)
+  const bool xp = tmpp != nullptr && (3 * C) % 32 == 0 && C % 8 == 0;
+  const uint16_t* tw = xp ? tmpp + (size_t)(kPad - 1) * C : nullptr;  // the window one row above
   launch_groupnorm_stats(x, lv.seg, B, C, 32, 1e-6f, stats, s);
-  launch_groupnorm_swish(x, lv.seg, B, lv.max_T, C, 32, stats, rb.n1w, rb.n1b, tmp, s);
+  launch_groupnorm_swish(x, lv.seg, B, lv.max_T, C, 32, stats, rb.n1w, rb.n1b, tmp, s, xp ? tmpp : nullptr, tplane);
   // conv1 (k=3, pad=1): sliding window starting one row above
-  gemm(tr - C, lv.M, 3 * C, C, rb.c1w, C, rb.c1b, orow, C, nullptr, 0, s);
+  if (xp) gemm_p(tw, tplane, lv.M, 3 * C, C, rb.c1w, C, rb.c1b, orow, C, nullptr, 0, s);
+  else gemm(tr - C, lv.M, 3 * C, C, rb.c1w, C, rb.c1b, orow, C, nullptr, 0, s);
   launch_groupnorm_stats(out, lv.seg, B, C, 32, 1e-6f, stats, s);
-  launch_groupnorm_swish(out, lv.seg, B, lv.max_T, C, 32, stats, rb.n2w, rb.n2b, tmp, s);
-  gemm(tr - C, lv.M, 3 * C, C, rb.c2w, C, rb.c2b, orow, C, xr, 0, s);  // x + h
+  launch_groupnorm_swish(out, lv.seg, B, lv.max_T, C, 32, stats, rb.n2w, rb.n2b, tmp, s, xp ? tmpp : nullptr,
+                         tplane);
+  if (xp) gemm_p(tw, tplane, lv.M, 3 * C, C, rb.c2w, C, rb.c2b, orow, C, xr, 0, s);  // x + h
+  else gemm(tr - C, lv.M, 3 * C, C, rb.c2w, C, rb.c2b, orow, C, xr, 0, s);
 }
 
 void grow(DevBuf& b, size_t bytes) {
@@ -423,6 +445,15 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
   grow(cd.head, (size_t)LF.rows * cd.ldh * 4);
   grow(cd.spec, (size_t)LF.rows * cd.ldh * 4);
   grow(cd.frames, (size_t)LF.rows * cd.nfft * 4);
+  const bool xp = use_x3p();
+  const long long p2 = (long long)max_rows * D, pbig = (long long)L0.rows * 4 * D;  // plane strides
+  if (xp) {
+    grow(cd.b2p, (size_t)p2 * 3 * 2);
+    grow(cd.bigpp, (size_t)pbig * 3 * 2);
+  }
+  uint16_t* b2p = xp ? cd.b2p.as<uint16_t>() : nullptr;
+  uint16_t* bigpp = xp ? cd.bigpp.as<uint16_t>() : nullptr;
+  auto RP = [&](uint16_t* buf, int C) { return buf + (size_t)kPad * C; };
 
   t_codec = &cd;
   float* b0 = cd.b0.as<float>();
@@ -433,17 +464,39 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
   auto R = [&](float* buf, int C) { return buf + (size_t)kPad * C; };
   // FSQ -> project_out -> fc_post_a; the embed conv reads zero gaps
   launch_fsq_project(codes_dev, (const int*)(mb + row_o), (int)code_row.size(), cd.po_w, cd.po_b, bigp, VQ, s);
-  gemm(R(bigp, VQ), L0.M, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, s);
-  launch_zero_gaps(b0, D, L0.seg, B, s);
-  // embed Conv1d(k=7, pad=3): window starts 3 rows above
-  gemm(R(b0, D) - 3 * D, L0.M, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, s);
+  if (xp) {  // fc_post_a writes the embed conv's planes (b2p holds them until the first resnet)
+    GemmF32Args g;
+    g.A = R(bigp, VQ); g.M = L0.M; g.K = VQ; g.lda = VQ; g.B = cd.fc_w; g.N = D; g.bias = cd.fc_b;
+    g.Bp = cd.bplanes.at(cd.fc_w);
+    g.C = nullptr; g.ldc = D; g.Cp = RP(b2p, D); g.cp_plane = p2;
+    launch_gemm_f32(g, s);
+    launch_zero_gaps(nullptr, D, L0.seg, B, s, b2p, p2);
+    gemm_p(RP(b2p, D) - 3 * D, p2, L0.M, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, s);
+  } else {
+    gemm(R(bigp, VQ), L0.M, VQ, VQ, cd.fc_w, D, cd.fc_b, R(b0, D), D, nullptr, 0, s);
+    launch_zero_gaps(b0, D, L0.seg, B, s);
+    // embed Conv1d(k=7, pad=3): window starts 3 rows above
+    gemm(R(b0, D) - 3 * D, L0.M, 7 * D, D, cd.emb_w, D, cd.emb_b, R(b1, D), D, nullptr, 0, s);
+  }
   // prior_net: b1 -> b0 -> b1
-  resnet(cd.prior[0], b1, b2, b0, L0, B, stats, s);
-  resnet(cd.prior[1], b0, b2, b1, L0, B, stats, s);
+  resnet(cd.prior[0], b1, b2, b0, L0, B, stats, s, b2p, p2);
+  resnet(cd.prior[1], b0, b2, b1, L0, B, stats, s, b2p, p2);
   // transformers on x = b1 (in place residual stream), scratch b2 / big / qkv
   float* x = R(b1, D);
   float* qkv = cd.qkv.as<float>();
-  for (int l = 0; l < c.depth; ++l) {
+  for (int l = 0; l < c.depth && xp; ++l) {
+    // the planes form: every GEMM input written as planes by its producer (gemm_x3p)
+    const CodecTfBlock& tb = cd.tf[l];
+    launch_rmsnorm_f32(x, L0.M, D, tb.att_norm, 1e-6f, nullptr, s, RP(b2p, D), p2);
+    gemm_p(RP(b2p, D), p2, L0.M, D, D, tb.c_attn, 3 * D, nullptr, R(qkv, 3 * D), 3 * D, nullptr, 0, s);
+    launch_codec_attention(qkv, L0.seg, (const int2*)(mb + qb_o), (int)qblk.size(), H, D / H, cd.rope_cs.as<float>(),
+                           b2, s, b2p, p2);
+    gemm_p(RP(b2p, D), p2, L0.M, D, D, tb.c_proj, D, nullptr, x, D, x, 0, s);
+    launch_rmsnorm_f32(x, L0.M, D, tb.ffn_norm, 1e-6f, nullptr, s, RP(b2p, D), p2);
+    gemm_p(RP(b2p, D), p2, L0.M, D, D, tb.fc1, 4 * D, nullptr, nullptr, 4 * D, nullptr, 1, s, RP(bigpp, 4 * D), pbig);
+    gemm_p(RP(bigpp, 4 * D), pbig, L0.M, 4 * D, 4 * D, tb.fc2, D, nullptr, x, D, x, 0, s);
+  }
+  for (int l = 0; l < c.depth && !xp; ++l) {
     const CodecTfBlock& tb = cd.tf[l];
     launch_rmsnorm_f32(x, L0.M, D, tb.att_norm, 1e-6f, R(b2, D), s);
     gemm(R(b2, D), L0.M, D, D, tb.c_attn, 3 * D, nullptr, R(qkv, 3 * D), 3 * D, nullptr, 0, s);
@@ -456,8 +509,8 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
     gemm(R(bigp, 4 * D), L0.M, 4 * D, 4 * D, tb.fc2, D, nullptr, x, D, x, 0, s);
   }
   // post_net: b1 -> b0 -> b1
-  resnet(cd.post[0], b1, b2, b0, L0, B, stats, s);
-  resnet(cd.post[1], b0, b2, b1, L0, B, stats, s);
+  resnet(cd.post[0], b1, b2, b0, L0, B, stats, s, b2p, p2);
+  resnet(cd.post[1], b0, b2, b1, L0, B, stats, s, b2p, p2);
   launch_layernorm_f32(R(b1, D), L0.M, D, cd.ln_w, cd.ln_b, 1e-6f, R(b0, D), s);
   float* hid = R(b0, D);
   int C = D;
@@ -471,7 +524,7 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
     launch_convt_gather(bigp, lv[i].seg, lv[i + 1].seg, B, lv[i + 1].max_T, u.Cout, u.k, u.u, u.pad, u.bias, nxt, s);
     C = u.Cout;
     float* res_out = (nxt == b0) ? b1 : b0;
-    resnet(u.rb, nxt, b2, res_out, lv[i + 1], B, stats, s);
+    resnet(u.rb, nxt, b2, res_out, lv[i + 1], B, stats, s, b2p, p2);
     cur = res_out;
   }
   if (NU > 0) {

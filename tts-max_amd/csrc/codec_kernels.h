@@ -30,6 +30,10 @@ struct GemmF32Args {
   int ldc = 0;
   const float* resid = nullptr;  // [M][ldc]
   int act = 0;                   // 0 none, 1 swish/silu
+  // optional output as bf16 planes for a consuming GEMM (gemm_x3p): element (m, n) of plane p
+  // at Cp + p * cp_plane + m * ldc + n (C may then be null)
+  uint16_t* Cp = nullptr;
+  long long cp_plane = 0;
   // split-K over workgroups (fp32 partials [ksplit][M][N] in `part`, summed in split order by
   // a reduce kernel): kept by the kernels, never used by launch_gemm_f32 (M-independent sums)
   float* part = nullptr;
@@ -37,6 +41,9 @@ struct GemmF32Args {
   int ksplit = 1, kchunk = 0;
 };
 void launch_gemm_f32(const GemmF32Args& g, hipStream_t s);
+// the same contraction with A and B both given as planes (Ap, Bp; codec_gemm.hip)
+bool gemm_x3p_supported(const GemmF32Args& g);
+void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s);
 // planes[0..3n) = the (h, m, l) bf16 split of x[0..n) the GEMM applies to its operands
 void launch_split_planes(const float* x, uint16_t* planes, long long n, hipStream_t s);
 
@@ -45,16 +52,19 @@ void launch_split_planes(const float* x, uint16_t* planes, long long n, hipStrea
 void launch_fsq_project(const int* codes, const int* code_row, int n, const float* w, const float* b,
                         float* out, int vq_dim, hipStream_t s);
 // zero the kCodecPad rows before the first and after every utterance of a ragged buffer
-void launch_zero_gaps(float* x, int C, const CodecSeg* seg, int B, hipStream_t s);
+void launch_zero_gaps(float* x, int C, const CodecSeg* seg, int B, hipStream_t s, uint16_t* xp = nullptr,
+                      long long plane = 0);
 // GroupNorm(32, eps) statistics of each utterance (stats [B][groups][mean, rstd])
 void launch_groupnorm_stats(const float* x, const CodecSeg* seg, int B, int C, int groups, float eps,
                             float* stats, hipStream_t s);
-// y = swish(GN(x)*gamma + beta) per utterance; y's gap rows are zeroed (a Conv1d input)
+// y = swish(GN(x)*gamma + beta) per utterance; y's gap rows are zeroed (a Conv1d input).
+// With yp: y's bf16 planes (gemm_x3p's A operand, element offsets of y) instead of y
 void launch_groupnorm_swish(const float* x, const CodecSeg* seg, int B, int max_T, int C, int groups,
-                            const float* stats, const float* gamma, const float* beta, float* y, hipStream_t s);
+                            const float* stats, const float* gamma, const float* beta, float* y, hipStream_t s,
+                            uint16_t* yp = nullptr, long long plane = 0);
 // codec RMSNorm (decoder_modules.py:226-236): x * rsqrt(mean(x^2) + eps) * w
 void launch_rmsnorm_f32(const float* x, int T, int C, const float* w, float eps, float* y,
-                        hipStream_t s);
+                        hipStream_t s, uint16_t* yp = nullptr, long long plane = 0);
 // LayerNorm over channels with affine
 void launch_layernorm_f32(const float* x, int T, int C, const float* w, const float* b, float eps,
                           float* y, hipStream_t s);
@@ -65,7 +75,8 @@ void launch_layernorm_f32(const float* x, int T, int C, const float* w, const fl
 int codec_attn_qblocks(int T);
 int codec_attn_qrows();  // queries per block (first query of block q = q * codec_attn_qrows())
 void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
-                            int hd, const float* rope_cs, float* out, hipStream_t s);
+                            int hd, const float* rope_cs, float* out, hipStream_t s, uint16_t* outp = nullptr,
+                            long long plane = 0);
 // rope_cs [heads][hd/2][cos, sin] of that rotation (once, at load)
 void launch_codec_rope_table(float* rope_cs, int heads, hipStream_t s);
 // ConvTranspose1d gather per utterance: y[t'][co] = b[co] + sum_j Z[(t'+pad-j)/u][j*Cout+co]

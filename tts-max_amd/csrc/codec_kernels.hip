@@ -18,6 +18,16 @@
 
 namespace tts {
 
+// one fp32 value as its three bf16 planes (element o of plane p at q + p * plane + o): the
+// split gemm_bx3_kernel applies while staging, written by the producer for gemm_x3p
+TTS_DEV void store_planes(uint16_t* __restrict__ q, long long plane, size_t o, float v) {
+  const float h = rbf(v), r = v - h, m = rbf(r);
+  q[o] = f2bf(h);
+  q[plane + o] = f2bf(m);
+  q[2 * plane + o] = f2bf(r - m);
+}
+
+
 // ------------------------------------------------------------------ fp32 MFMA GEMM ----
 // Tile TM x TN x 16, four waves in a 2x2 grid, each wave (TM/2) x (TN/2) built from
 // 32x32 v_mfma_f32_32x32x2_f32 tiles.  Operands are staged k-major in LDS (row stride
@@ -132,7 +142,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32Args g) {
         float v = acc[i][j][r] + bias;
         if (g.act == 1) v = v / (1.0f + expf(-v));
         if (g.resid) v = g.resid[(size_t)m * g.ldc + n] + v;
-        g.C[(size_t)m * g.ldc + n] = v;
+        if (g.C) g.C[(size_t)m * g.ldc + n] = v;
+        if (g.Cp) store_planes(g.Cp, g.cp_plane, (size_t)m * g.ldc + n, v);
       }
   }
 }
@@ -390,7 +401,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
         float v = acc[i][j][r] + bias;
         if (g.act == 1) v = v / (1.0f + expf(-v));
         if (g.resid) v = g.resid[(size_t)m * g.ldc + n] + v;
-        g.C[(size_t)m * g.ldc + n] = v;
+        if (g.C) g.C[(size_t)m * g.ldc + n] = v;
+        if (g.Cp) store_planes(g.Cp, g.cp_plane, (size_t)m * g.ldc + n, v);
       }
   }
 }
@@ -477,15 +489,23 @@ void launch_fsq_project(const int* codes, const int* code_row, int n, const floa
 
 // The zero rows around the utterances of a ragged buffer (the padding a Conv1d window
 // reads): kPad rows before the first and after every utterance.
-__global__ void zero_gaps_kernel(float* __restrict__ x, int C, const CodecSeg* __restrict__ seg) {
+__global__ void zero_gaps_kernel(float* __restrict__ x, int C, const CodecSeg* __restrict__ seg,
+                                 uint16_t* __restrict__ xp, long long plane) {
   const int g = blockIdx.x;
   const size_t r0 = g == 0 ? 0 : (size_t)(seg[g - 1].row + seg[g - 1].T);
-  float* p = x + r0 * C;
-  for (int i = threadIdx.x; i < kCodecPad * C; i += blockDim.x) p[i] = 0.f;
+  for (int i = threadIdx.x; i < kCodecPad * C; i += blockDim.x) {
+    if (xp) {  // (the buffer's planes: all three are +0)
+      xp[r0 * C + i] = 0;
+      xp[plane + r0 * C + i] = 0;
+      xp[2 * plane + r0 * C + i] = 0;
+    } else {
+      x[r0 * C + i] = 0.f;
+    }
+  }
 }
 
-void launch_zero_gaps(float* x, int C, const CodecSeg* seg, int B, hipStream_t s) {
-  hipLaunchKernelGGL(zero_gaps_kernel, dim3(B + 1), dim3(256), 0, s, x, C, seg);
+void launch_zero_gaps(float* x, int C, const CodecSeg* seg, int B, hipStream_t s, uint16_t* xp, long long plane) {
+  hipLaunchKernelGGL(zero_gaps_kernel, dim3(B + 1), dim3(256), 0, s, x, C, seg, xp, plane);
 }
 
 // GroupNorm statistics (torch.nn.GroupNorm, biased variance), two passes in fp32.
@@ -531,47 +551,60 @@ void launch_groupnorm_stats(const float* x, const CodecSeg* seg, int B, int C, i
 __global__ void groupnorm_swish_kernel(const float* __restrict__ x_all, const CodecSeg* __restrict__ seg,
                                        int C, int cg, int groups, const float* __restrict__ stats_all,
                                        const float* __restrict__ gamma,
-                                       const float* __restrict__ beta, float* __restrict__ y_all) {
+                                       const float* __restrict__ beta, float* __restrict__ y_all,
+                                       uint16_t* __restrict__ yp, long long plane) {
   const int b = blockIdx.y;
   const size_t row = (size_t)seg[b].row;
   const long long n = (long long)seg[b].T * C;
   const float* x = x_all + row * C;
-  float* y = y_all + row * C;
   const float* stats = stats_all + (size_t)b * groups * 2;
+  // (yp: the conv GEMM's planes instead of fp32 y; same element offsets)
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C), grp = c / cg;
     const float v = (x[i] - stats[2 * grp]) * stats[2 * grp + 1] * gamma[c] + beta[c];
-    y[i] = v / (1.0f + expf(-v));
+    const float o = v / (1.0f + expf(-v));
+    if (yp) store_planes(yp, plane, row * C + i, o);
+    else y_all[row * C + i] = o;
   }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)kCodecPad * C;
        i += (long long)gridDim.x * blockDim.x) {
-    y[n + i] = 0.f;
-    if (b == 0) y_all[i] = 0.f;
+    if (yp) {
+      store_planes(yp, plane, row * C + n + i, 0.f);
+      if (b == 0) store_planes(yp, plane, i, 0.f);
+    } else {
+      y_all[row * C + n + i] = 0.f;
+      if (b == 0) y_all[i] = 0.f;
+    }
   }
 }
 
 void launch_groupnorm_swish(const float* x, const CodecSeg* seg, int B, int max_T, int C, int groups,
-                            const float* stats, const float* gamma, const float* beta, float* y, hipStream_t s) {
+                            const float* stats, const float* gamma, const float* beta, float* y, hipStream_t s,
+                            uint16_t* yp, long long plane) {
   const long long n = (long long)max_T * C;
   int grid = (int)std::min<long long>((n + 255) / 256, std::max(1, 8192 / B));
   hipLaunchKernelGGL(groupnorm_swish_kernel, dim3(grid, B), dim3(256), 0, s, x, seg, C, C / groups, groups,
-                     stats, gamma, beta, y);
+                     stats, gamma, beta, y, yp, plane);
 }
 
 __global__ void rmsnorm_f32_kernel(const float* __restrict__ x, int C, const float* __restrict__ w,
-                                   float eps, float* __restrict__ y) {
+                                   float eps, float* __restrict__ y, uint16_t* __restrict__ yp, long long plane) {
   __shared__ float red[16];
   const float* xr = x + (size_t)blockIdx.x * C;
   float ss = 0.f;
   for (int c = threadIdx.x; c < C; c += blockDim.x) ss += xr[c] * xr[c];
   const float r = 1.0f / sqrtf(block_sum(ss, red) / (float)C + eps);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) y[(size_t)blockIdx.x * C + c] = xr[c] * r * w[c];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float v = xr[c] * r * w[c];
+    if (yp) store_planes(yp, plane, (size_t)blockIdx.x * C + c, v);  // (the GEMM's planes)
+    else y[(size_t)blockIdx.x * C + c] = v;
+  }
 }
 
 void launch_rmsnorm_f32(const float* x, int T, int C, const float* w, float eps, float* y,
-                        hipStream_t s) {
-  hipLaunchKernelGGL(rmsnorm_f32_kernel, dim3(T), dim3(256), 0, s, x, C, w, eps, y);
+                        hipStream_t s, uint16_t* yp, long long plane) {
+  hipLaunchKernelGGL(rmsnorm_f32_kernel, dim3(T), dim3(256), 0, s, x, C, w, eps, y, yp, plane);
 }
 
 // (x and y may alias: callers normalise in place; each thread rewrites only elements it read)
@@ -671,7 +704,8 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
                                                          const CodecSeg* __restrict__ seg,
                                                          const int2* __restrict__ qblk, int heads,
                                                          const float2* __restrict__ rope_cs,
-                                                         float* __restrict__ out_all, int expf_mode) {
+                                                         float* __restrict__ out_all, int expf_mode,
+                                                         uint16_t* __restrict__ outp, long long plane) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ks = (bf16_t*)smem;                 // [3][64 keys][APL]
   bf16_t* Vt = Ks + 3 * 64 * APL;             // [3][64 d][APL]
@@ -859,7 +893,11 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
     if (q >= T) continue;
     const float inv = 1.0f / lrow[r];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) out[(size_t)q * W + h * AD + 16 * dt + c16] = o[dt][r] * inv;
+    for (int dt = 0; dt < 4; ++dt) {
+      const size_t oi = (size_t)q * W + h * AD + 16 * dt + c16;
+      if (outp) store_planes(outp, plane, (size_t)seg[qb.x].row * W + oi, o[dt][r] * inv);  // (c_proj's planes)
+      else out[oi] = o[dt][r] * inv;
+    }
   }
 }
 
@@ -872,7 +910,7 @@ int codec_attn_qrows() { return 16 * attn_waves(); }
 int codec_attn_qblocks(int T) { return (T + codec_attn_qrows() - 1) / codec_attn_qrows(); }
 
 void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* qblk, int nqblk, int heads,
-                            int hd, const float* rope_cs, float* out, hipStream_t s) {
+                            int hd, const float* rope_cs, float* out, hipStream_t s, uint16_t* outp, long long plane) {
   if (hd != AD) throw std::runtime_error("codec attention: head_dim 64 expected");
   dim3 grid(nqblk, heads);
   // libm expf by default: the base-2 v_exp_f32 form measured neutral here (32 x 650 codes 62.0 ms
@@ -881,10 +919,10 @@ void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* q
   static const int expf_mode = getenv("TTS_CODEC_EXPF") ? atoi(getenv("TTS_CODEC_EXPF")) : 1;
   if (attn_waves() == 8)
     hipLaunchKernelGGL(codec_attn_kernel<8>, grid, dim3(512), attn_lds(8), s, qkv, seg, qblk, heads,
-                       (const float2*)rope_cs, out, expf_mode);
+                       (const float2*)rope_cs, out, expf_mode, outp, plane);
   else
     hipLaunchKernelGGL(codec_attn_kernel<4>, grid, dim3(256), attn_lds(4), s, qkv, seg, qblk, heads,
-                       (const float2*)rope_cs, out, expf_mode);
+                       (const float2*)rope_cs, out, expf_mode, outp, plane);
 }
 
 // (cos, sin) of the torchtune rotation for every (head h, pair p): angle h * 10000^(-2p/64),

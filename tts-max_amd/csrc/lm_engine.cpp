@@ -130,6 +130,10 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
                   (c.num_heads * c.head_dim) % 256 == 0,
               "hidden/intermediate/attention widths must be multiples of 256");
   TTS_REQUIRE(c.vocab_size % 16 == 0, "vocab_size must be a multiple of 16");
+  // (the GEMMs stream a matrix through one buffer resource: 32-bit byte offsets)
+  TTS_REQUIRE((double)c.vocab_size * c.hidden_size * 2 < 4.0e9 &&
+                  (double)2 * c.intermediate_size * c.hidden_size * 2 < 4.0e9,
+              "a weight matrix of 4 GB or more is not supported");
   TTS_REQUIRE(c.max_batch >= 1 && c.max_batch <= 64, "max_batch must be in [1, 64]");
   TTS_REQUIRE(c.max_seq_len >= 16, "max_seq_len too small");
   TensorMap tm;

@@ -471,10 +471,18 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   }
 
   // ---- then the weight stream
-  // stage st of the wave's item of unit uu: NG*KU consecutive tiles (StreamPlan layout)
-  auto sptr = [&](int uu, int st) {
+  // Buffer loads through one resource over the whole tiled matrix (32-bit offsets: no 64-bit
+  // address per load).  A refill past the wave's last unit gets an offset beyond the
+  // resource's range: the load returns zeros without touching memory, so every unit runs the
+  // same consume-and-refill loop (no separate drain path) and the ring registers never need
+  // path-merging copies (each such copy of an in-flight register is a vmcnt wait, i.e. the
+  // ring drained at every unit boundary).
+  const uint32_t wbytes = (uint32_t)((long long)(a.N >> 4) * KT * 1024);  // (< 4 GiB: host-checked)
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)wbytes, 0x00020000);
+  // byte offset of this lane's 16 B of stage st of the wave's item of unit uu (NG*KU tiles)
+  auto soff = [&](int uu, int st) -> uint32_t {
     const int ls = cs2 ? ((lane & ~8) | ((min(uu, units - 1) & 1) << 3)) : lane;
-    return (const u32x4_t*)a.w + stile(uu, st) * 64 + ls;
+    return uu < units ? (uint32_t)stile(uu, st) * 1024u + (uint32_t)ls * 16u : 0xFFFFFFF0u;
   };
   // Register ring of R stages (S = stages per item, S % R == 0): the first R stages of the
   // wave's stream are in flight before the prologue runs; consuming a slot refills it with
@@ -488,16 +496,16 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   const int akoff = 8 * (lane >> 4);
   u32x4_t ar[R][KU][AGR ? MT_MAX : 1];
   int pu = u, ps = 0;  // next stage to issue
-  // The refills are issued only where the stage exists by construction (never behind a
-  // per-iteration condition): every path then has a fixed load count and the compiler's
-  // vmcnt waits stay exact (a conditional issue makes it merge paths pessimistically,
-  // i.e. drain the ring at every stage).
+  // The refills are unconditional (past the wave's last unit: the out-of-range offset): every
+  // path then has a fixed load count and the compiler's vmcnt waits stay exact (a conditional
+  // issue makes it merge paths pessimistically, i.e. drain the ring at every stage).
   auto issue = [&](u32x4_t (&dst)[KU][NG], u32x4_t (&adst)[KU][AGR ? MT_MAX : 1]) {
-    const u32x4_t* q = sptr(pu, ps);
+    const uint32_t q = soff(pu, ps);
 #pragma unroll
     for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
-      for (int g = 0; g < NG; ++g) dst[kk][g] = __builtin_nontemporal_load(q + (g * KU + kk) * 64);
+      for (int g = 0; g < NG; ++g)  // (aux 2: the non-temporal policy: streamed once per step)
+        dst[kk][g] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, (int)(q + (uint32_t)((g * KU + kk) * 1024)), 0, 2);
     if constexpr (AGR) {
       const int sg = ps + st_off, ch = kc == 1 ? 0 : sg / Sc;
       const int kt = ch * KTc + kpart * kt_pc + (sg - ch * Sc) * KU - kt_base;
@@ -516,8 +524,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // (each prologue wait would then drain the primed stages too)
   __builtin_amdgcn_sched_barrier(0);
   if (a.diag & kWgemmDiagMask & 8) __syncthreads();
-  // (unconditional: a wave with no unit streams unit units-1, never consumed (sptr clamps).
-  // A branch here would make every prologue wait below drain the primed stages as well)
+  // (unconditional: a wave with no unit issues out-of-range loads, never consumed.  A branch
+  // here would make every prologue wait below drain the primed stages as well)
 #pragma unroll
   for (int j = 0; j < R; ++j) issue(wr[j], ar[j]);
   __builtin_amdgcn_sched_barrier(0);
@@ -657,18 +665,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       consume(wr[j], ar[j], stage);
       issue(wr[j], ar[j]);
     };
-    if (u + ustride < units) {  // the wave has a next unit: every refill exists
-      for (int st = 0; st < S; st += R) {
+    // one loop for every unit (the last one's refills are the out-of-range loads)
+    for (int st = 0; st < S; st += R) {
 #pragma unroll
-        for (int j = 0; j < R; ++j) step(j, st + j);
-      }
-    } else {  // last unit of the wave (or none): refill while stages remain, then drain
-      for (int st = 0; st + R < S; st += R) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) step(j, st + j);
-      }
-#pragma unroll
-      for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j);
+      for (int j = 0; j < R; ++j) step(j, st + j);
     }
 
     if (first) { TTS_STAMP(stp, 2); TTS_STAMP_WAVE(stp, 8 + wave); }
