@@ -323,6 +323,12 @@ bool use_kslice32() {
   static const bool v = !(getenv("TTS_KSLICE32") && !atoi(getenv("TTS_KSLICE32")));
   return v;
 }
+// ... for the residual projection (o_proj) alone: TTS_KSLICE32_RESID=0 runs it unsliced (the A
+// rows staged whole, the residual epilogue writes the hidden rows: no combine launch)
+bool use_kslice32_resid() {
+  static const bool v = !(getenv("TTS_KSLICE32_RESID") && !atoi(getenv("TTS_KSLICE32_RESID")));
+  return v;
+}
 // ... and at 2..16 rows, o_proj fused behind the attention of the QKV launch (its own
 // workgroups after the attention's): default on; TTS_FUSED_OPROJ_ROWS=0 keeps the launch
 bool use_fused_oproj_rows() {
@@ -402,8 +408,8 @@ struct Ctx {
       // add + the next RMSNorm (the gate/up prologue's norm) in one pass.  TTS_KSLICE32=0: off
       // (chosen by the batch's row count, not the chunk's: a 33..64-row batch runs two chunks,
       // and every row of a batch must take the same arithmetic)
-      if (!norm && rows > 16 && m <= 32 && K == 2048 && !logit_extra && (epi == EPI_STORE || epi == EPI_RESID) &&
-          use_kslice32() && p.sp.kc == 1 && p.sp.waves == 16 && p.sp.ksplit == 16 && p.sp.ku == 2 && p.sp.ng == 1 &&
+      if (!norm && rows > 16 && m <= 32 && K == 2048 && !logit_extra &&
+          (epi == EPI_STORE || (epi == EPI_RESID && use_kslice32_resid())) && use_kslice32() && p.sp.kc == 1 && p.sp.waves == 16 && p.sp.ksplit == 16 && p.sp.ku == 2 && p.sp.ng == 1 &&
           (size_t)4 * m * ldo * 4 <= w.kpart.bytes) {
         WgemmArgs a;
         a.x = xin; a.M = m; a.K = K / 4; a.ldx = K;
