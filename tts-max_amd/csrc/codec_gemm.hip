@@ -115,42 +115,56 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto bf = [](const u32x4_t& x) { return __builtin_bit_cast(bf16x8_t, x); };
+  // the 3 (MI + NJ) fragments of k-slice kk of the stage at LDS byte address sb
+  auto read_frags = [&](uint32_t sb, int kk, u32x4_t (&a)[3][MI], u32x4_t (&b)[3][NJ]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p][i] = lds_rd16(sb + aoff[kk][i] + p * APL);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[p][j] = lds_rd16(sb + boff[kk][j] + p * BPL);
+  };
+  // the reads' results are used only after this wait: each fragment passes through an (empty)
+  // volatile asm after it, which the compiler keeps in order behind the wait
+  auto land_frags = [&](u32x4_t (&a)[3][MI], u32x4_t (&b)[3][NJ]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[p][i]));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(b[p][j]));
+    }
+  };
+  auto mfmas = [&](const u32x4_t (&a)[3][MI], const u32x4_t (&b)[3][NJ]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        f32x16_t c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[1][i]), bf(b[1][j]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[2][i]), bf(b[0][j]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[2][j]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[1][i]), bf(b[0][j]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[1][j]), c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[0][j]), c, 0, 0, 0);
+      }
+  };
+  // one stage: k-slice 1's fragment reads are issued before k-slice 0's MFMAs (the scheduling
+  // barrier keeps them there), so their LDS latency hides under those MFMAs
   auto compute = [&](int buf) {
     const uint32_t sb = l0 + buf * STAGE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x4_t a[3][MI], b[3][NJ];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) a[p][i] = lds_rd16(sb + aoff[kk][i] + p * APL);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b[p][j] = lds_rd16(sb + boff[kk][j] + p * BPL);
-      // the reads' results are used only after this wait: each fragment passes through an
-      // (empty) volatile asm after it, which the compiler keeps in order behind the wait
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[p][i]));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(b[p][j]));
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          f32x16_t c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[1][i]), bf(b[1][j]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[2][i]), bf(b[0][j]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[2][j]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[1][i]), bf(b[0][j]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[1][j]), c, 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[0][j]), c, 0, 0, 0);
-        }
-    }
+    u32x4_t a0[3][MI], b0[3][NJ], a1[3][MI], b1[3][NJ];
+    read_frags(sb, 0, a0, b0);
+    land_frags(a0, b0);
+    read_frags(sb, 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    land_frags(a1, b1);
+    mfmas(a1, b1);
   };
 
   // ---- two stages in flight; stage s is read after its DMA was counted in and every wave
@@ -193,6 +207,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
           const size_t o = (size_t)m * g.ldc + n;
           if (g.C) g.C[o] = v;
           if (g.Cp) {  // the consumer GEMM's planes (the split every producer uses)
+            asm("" : "+v"(v));  // (no contraction into v - h: see store_planes)
             const float h = rbf(v), rm = v - h, mm = rbf(rm);
             g.Cp[o] = f2bf(h);
             g.Cp[g.cp_plane + o] = f2bf(mm);

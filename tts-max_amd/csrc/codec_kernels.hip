@@ -21,6 +21,9 @@ namespace tts {
 // one fp32 value as its three bf16 planes (element o of plane p at q + p * plane + o): the
 // split gemm_bx3_kernel applies while staging, written by the producer for gemm_x3p
 TTS_DEV void store_planes(uint16_t* __restrict__ q, long long plane, size_t o, float v) {
+  // (v as the fp32 value a store would hold: the compiler must not contract the product that
+  // made v into v - h, or the planes would split a value the fp32 path never sees)
+  asm("" : "+v"(v));
   const float h = rbf(v), r = v - h, m = rbf(r);
   q[o] = f2bf(h);
   q[plane + o] = f2bf(m);

@@ -53,8 +53,11 @@ TTS_DEV int dec_pos(int base, int mt, int row) {
 
 // One pass's fragments of this wave: kf = K rows (clamped to the last valid position; the
 // rows past ctx are masked), vf = V^T columns (clamped inside the stride).  Unconditional
-// loads: a fixed load count keeps the compiler's vmcnt waits exact.
-template <int D, int PW>
+// loads: a fixed load count keeps the compiler's vmcnt waits exact.  O32: 32-bit element
+// offsets inside the (slot, kv head) block (S * D < 2^31) — in the standalone kernel the 64-bit
+// ones stayed live across the passes in register pairs and spilled; the fused consumer
+// allocates best with the 64-bit form.  (Addresses only: the same bits either way.)
+template <int D, int PW, bool O32 = false>
 TTS_DEV void dec_load_k(const bf16_t* kc, int base, int ctx, int lane,
                         u32x4_t (&kf)[DecShape<D, PW>::MT][DecShape<D, PW>::KS]) {
   using C = DecShape<D, PW>;
@@ -63,10 +66,12 @@ TTS_DEV void dec_load_k(const bf16_t* kc, int base, int ctx, int lane,
   for (int mt = 0; mt < C::MT; ++mt) {
     const int p = min(dec_pos(base, mt, c), ctx - 1);
 #pragma unroll
-    for (int ks = 0; ks < C::KS; ++ks) kf[mt][ks] = *(const u32x4_t*)(kc + (size_t)p * D + 32 * ks + 8 * g);
+    for (int ks = 0; ks < C::KS; ++ks)
+      kf[mt][ks] = O32 ? *(const u32x4_t*)(kc + (p * D + 32 * ks + 8 * g))
+                       : *(const u32x4_t*)(kc + (size_t)p * D + 32 * ks + 8 * g);
   }
 }
-template <int D, int PW>
+template <int D, int PW, bool O32 = false>
 TTS_DEV void dec_load_v(const bf16_t* vtc, int S, int base, int lane,
                         u32x4_t (&vf)[DecShape<D, PW>::PS][DecShape<D, PW>::DT]) {
   using C = DecShape<D, PW>;
@@ -75,7 +80,9 @@ TTS_DEV void dec_load_v(const bf16_t* vtc, int S, int base, int lane,
   for (int ps = 0; ps < C::PS; ++ps) {
     const int p0 = min(base + 32 * ps + 8 * g, S - 8);
 #pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) vf[ps][dt] = *(const u32x4_t*)(vtc + (size_t)(16 * dt + c) * S + p0);
+    for (int dt = 0; dt < C::DT; ++dt)
+      vf[ps][dt] = O32 ? *(const u32x4_t*)(vtc + ((16 * dt + c) * S + p0))
+                       : *(const u32x4_t*)(vtc + (size_t)(16 * dt + c) * S + p0);
   }
 }
 
@@ -200,7 +207,7 @@ constexpr int dec_red_floats() { return NW * DEC_G * 2 + NW * DEC_G * D; }
 // output, bf16 [4][D] (row of attn_out at the group's first head).
 // (general form: `wave` / `tid` = this wave's / thread's index among the NW attending waves,
 // `bar` = a barrier over exactly those waves; dec_attend below: the whole workgroup)
-template <int D, int PW, int NW, class Bar>
+template <int D, int PW, int NW, class Bar, bool O32 = false>
 TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, float scale, const float* qs,
                           const bf16_t* knew, const bf16_t* vnew, float* red,
                           u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
@@ -233,7 +240,7 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
     const int base = (ps * NW + wave) * PW;
     if (base >= ctx) break;
     u32x4_t kf[C::MT][C::KS];
-    dec_load_k<D, PW>(kc, base, ctx, lane, kf);
+    dec_load_k<D, PW, O32>(kc, base, ctx, lane, kf);
     dec_patch_k<D, PW>(base, ctx, lane, knew, kf);
     f32x4_t s[C::MT];
     dec_scores<D, PW>(kf, qs, base, ctx, scale, lane, s);
@@ -261,8 +268,8 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
     const int base = (ps * NW + wave) * PW;
     if (base >= ctx) break;
     u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
-    dec_load_v<D, PW>(vtc, S, base, lane, vf);
-    dec_load_k<D, PW>(kc, base, ctx, lane, kf);
+    dec_load_v<D, PW, O32>(vtc, S, base, lane, vf);
+    dec_load_k<D, PW, O32>(kc, base, ctx, lane, kf);
     dec_patch_k<D, PW>(base, ctx, lane, knew, kf);
     f32x4_t s[C::MT];
     dec_scores<D, PW>(kf, qs, base, ctx, scale, lane, s);
@@ -307,15 +314,15 @@ TTS_DEV void dec_attend_w(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, f
   }
 }
 
-template <int D, int PW, int NW>
+template <int D, int PW, int NW, bool O32 = false>
 TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, float scale, const float* qs,
                         const bf16_t* knew, const bf16_t* vnew, float* red,
                         u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
                         u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], bf16_t* out,
                         unsigned long long* stp = nullptr, uint64_t* gout = nullptr, uint32_t gtag = 0) {
-  dec_attend_w<D, PW, NW>(kc, vtc, S, ctx, scale, qs, knew, vnew, red, kf0, vf0, out,
-                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, [] { lds_barrier(); }, stp,
-                          gout, gtag);
+  auto bar = [] { lds_barrier(); };
+  dec_attend_w<D, PW, NW, decltype(bar), O32>(kc, vtc, S, ctx, scale, qs, knew, vnew, red, kf0, vf0, out,
+                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, bar, stp, gout, gtag);
 }
 
 // ---------------------------------------------------- split decode attention (batched) -----

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <stdexcept>
+#include <type_traits>
 
 #include "hip_common.h"
 #include "lm_kernels.h"
@@ -23,6 +24,8 @@ __host__ __device__ inline int wgemm_red_floats(int waves, int ksplit, int ng, i
   const int segs = (M * (Kl / 8) + 63) / 64;
   r = r > segs ? r : segs;
   r = r > Kl / 2 ? r : Kl / 2;  // RMSNorm weight (bf16) parked here during the LDS-DMA prologue
+  const int wsg = Kl / 2 + M * (Kl / 512);  // ... followed by the [M][K / 512] segment sums
+  r = r > wsg ? r : wsg;
   return r + 64;
 }
 
@@ -581,20 +584,42 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     TTS_STAMP(stp, 6);  // (A rows landed)
     if (a.diag & kWgemmDiagMask & 16) {
     } else if constexpr (NORM) {
-      const bf16_t* gw = (const bf16_t*)red;
-      for (int m = wave; m < M; m += WAVES) {
-        bf16_t* xr = xs + (size_t)m * ldxs;
+      // RMSNorm of the landed rows, spread over every wave (a wave per row left half the
+      // waves idle and made each busy one scale a whole row: ~4 us at 8 rows of 4096):
+      // (a) the canonical segment sums (chunk_sumsq + the wave DPP tree over each 512-value
+      //     segment: the same bits as every other RMSNorm path) of all (row, segment) pairs;
+      // (b) each wave scales only the A columns it will read (its k-part's k-tiles) of every
+      //     row, the UPW waves sharing a k-part splitting them; r from the segments in order
+      const bf16_t* gw = (const bf16_t*)red;      // (the parked RMSNorm weight)
+      float* segs = red + (a.K >> 1);              // [M][K / 512] segment sums
+      const int nseg = a.K >> 9;
+      for (int p = wave; p < M * nseg; p += WAVES) {
+        const int m = p / nseg, sg = p - m * nseg;
+        const float sv = wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xs + (size_t)m * ldxs + sg * 512 + lane * 8)));
+        if (lane == 0) segs[p] = sv;
+      }
+      __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
+      __builtin_amdgcn_s_barrier();
+      // r of row m in lane m (M <= 64), read back uniformly (s_readlane) per row below
+      float rv = 0.f;
+      if (lane < M) {
         float ss = 0.f;
-        for (int k0 = 0; k0 < a.K; k0 += 512)  // canonical order (chunk_sumsq)
-          ss += wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xr + k0 + lane * 8)));
-        const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-        for (int k = lane * 8; k < a.K; k += 512) {
-          u32x4_t v = *(const u32x4_t*)(xr + k);
-          const u32x4_t g = *(const u32x4_t*)(gw + k);
+        for (int sg = 0; sg < nseg; ++sg) ss += segs[lane * nseg + sg];  // (segments in order)
+        rv = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+      }
+      const int Q = kc * kt_pc * 4;  // (k-tile, 8-column chunk) items of this k-part (non-sliced: kpart == kq)
+      for (int x = ugrp * 64 + lane; x < Q; x += UPW * 64) {
+        const int t = x >> 2, ch = t / kt_pc;
+        const int k = (ch * KTc + kq * kt_pc + (t - ch * kt_pc)) * 32 + (x & 3) * 8;
+        const u32x4_t g = *(const u32x4_t*)(gw + k);
+        for (int m = 0; m < M; ++m) {
+          const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), m));
+          bf16_t* xr = xs + (size_t)m * ldxs + k;
+          u32x4_t v = *(const u32x4_t*)xr;
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
-          *(u32x4_t*)(xr + k) = v;
+          *(u32x4_t*)xr = v;
         }
       }
       __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
@@ -619,7 +644,9 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     for (int r = 0; r < 4; ++r) { best_v[mt][r] = -INFINITY; best_i[mt][r] = 0x7fffffff; }
 
   bool first = true;
-  for (int ubase = bx * UPW; ubase < units; ubase += ustride) {
+  // the unit body: `single` (compile-time) = every wave of the launch has at most one unit, so
+  // the stream ends with the unit (no out-of-range refills, the last stages drained in place)
+  auto unit_body = [&](int ubase, auto single) {
     u = ubase + ugrp;
     const bool active = u < units;
     uint32_t seen_nxt[MT_MAX][4];
@@ -665,16 +692,24 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       consume(wr[j], ar[j], stage);
       issue(wr[j], ar[j]);
     };
-    // one loop for every unit (the last one's refills are the out-of-range loads)
-    for (int st = 0; st < S; st += R) {
+    if constexpr (decltype(single)::value) {  // the wave's only unit: refill while stages remain, then drain
+      for (int st = 0; st + R < S; st += R) {
 #pragma unroll
-      for (int j = 0; j < R; ++j) step(j, st + j);
+        for (int j = 0; j < R; ++j) step(j, st + j);
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) consume(wr[j], ar[j], S - R + j);
+    } else {  // one loop for every unit (the last one's refills are the out-of-range loads)
+      for (int st = 0; st < S; st += R) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) step(j, st + j);
+      }
     }
 
     if (first) { TTS_STAMP(stp, 2); TTS_STAMP_WAVE(stp, 8 + wave); }
     if (a.diag & kWgemmDiagMask & 2) {
       if (acc[0][0][0] == 1234.5f && a.out) a.out[0] = 0;
-      continue;
+      return;
     }
     // ---- split-K combine through LDS, fixed order (deterministic)
     if constexpr (KSW > 1) {
@@ -807,6 +842,11 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) seen_cur[mt][r] = seen_nxt[mt][r];
     }
+  };
+  if (units <= ustride) {
+    unit_body(bx * UPW, std::true_type{});
+  } else {
+    for (int ubase = bx * UPW; ubase < units; ubase += ustride) unit_body(ubase, std::false_type{});
   }
 
   if constexpr (FATT) {
