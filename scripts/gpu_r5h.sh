@@ -8,6 +8,13 @@ T=${1:-r5h}
 mkdir -p $O
 export TMPDIR=/tmp
 bash scripts/gpu_round.sh $T tests || exit $?
+for v in 0 1; do
+  for b in 32 1; do
+    TTS_CODEC_X3P_ILV=$v timeout -k 10 120 python scripts/codec_probe32.py $b 650 >> $O/${T}_ab_codec_ilv.txt 2>&1 || exit $?
+    echo "  (TTS_CODEC_X3P_ILV=$v)" >> $O/${T}_ab_codec_ilv.txt
+  done
+done
+cat $O/${T}_ab_codec_ilv.txt
 export AB_V0=$PWD/ablib/lib_cur.so AB_V1=$PWD/tts-max_amd/tts_amd/libtts_mi355x.so
 timeout -k 10 300 python scripts/env_ab_probe.py TTS_LIB_PATH 8 1 > $O/${T}_ab_8.txt 2>&1 || exit $?
 timeout -k 10 300 python scripts/env_ab_probe.py TTS_LIB_PATH 32 1 > $O/${T}_ab_32.txt 2>&1 || exit $?

@@ -587,6 +587,7 @@ void codec_decode(Engine* e, const int32_t* codes, const int32_t* lens, int B, f
   }
   if (!wav_is_device) HIP_CHECK(hipMemcpyAsync(wav, wav_dev, n_wav * 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  if (getenv("TTS_CODEC_STAMPS")) x3p_stamps_dump(stderr);  // (stamps build only)
 }
 
 }  // namespace tts

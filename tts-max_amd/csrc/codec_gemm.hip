@@ -22,6 +22,7 @@
 // only after its own DMA was counted in (vmcnt) and every wave passed the barrier, and it is
 // refilled only after every wave passed the barrier that ends its reads.
 #include <algorithm>
+#include <cstdio>
 #include <stdexcept>
 
 #include "codec_kernels.h"
@@ -31,6 +32,16 @@ namespace tts {
 
 typedef __attribute__((address_space(3))) char lds_char_t;
 
+#ifdef TTS_STAMPS
+// diagnostic build only: per-wave shader-clock sums of the K loop's phases, over every launch
+// (x3p_stamps_dump: [0] wait + barrier, [1] kk0 fragments landing, [2] MFMA phase, [3] epilogue,
+// [4] whole wave, [5] waves)
+__device__ unsigned long long g_x3p_cyc[8];
+#define X3P_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define X3P_T(v) do {} while (0)
+#endif
+
 // one 16-B LDS read (inline asm: invisible to the compiler's LDS-DMA alias waits)
 TTS_DEV u32x4_t lds_rd16(uint32_t addr) {
   u32x4_t v;
@@ -38,7 +49,7 @@ TTS_DEV u32x4_t lds_rd16(uint32_t addr) {
   return v;
 }
 
-template <int TM, int TN, int WM, int WN>
+template <int TM, int TN, int WM, int WN, bool ILV>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int MI = TM / WM / 32, NJ = TN / WN / 32;  // 32x32 accumulators per wave
@@ -48,9 +59,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   constexpr int APL = TM * 64, BPL = TN * 64;            // bytes of one plane's stage image
   constexpr int STAGE = 3 * (APL + BPL);
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  X3P_T(t_entry);
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave / WN, wn = wave % WN;
+#ifdef TTS_STAMPS
+  unsigned long long c_wait = 0, c_land = 0, c_mfma = 0;
+#endif
   // XCD-aware tile order: consecutive blocks land on the 8 XCDs in turn, so tile id
   // (b % 8) * (tiles / 8) + b / 8 gives each XCD a contiguous run of tiles, i.e. the N tiles
   // of the same A rows share that XCD's L2
@@ -81,11 +96,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
     }
   }
   lds_char_t* lbase = (lds_char_t*)smem;
+  auto issue1 = [&](int j, int s, int buf) {
+    __builtin_amdgcn_global_load_lds((gptr_t)(srcp[j] + s * 32), (lptr_t)(lbase + buf * STAGE + dstoff[j]), 16, 0, 0);
+  };
   auto issue = [&](int s, int buf) {
-    const int k0 = s * 32;
 #pragma unroll
-    for (int j = 0; j < QW; ++j)
-      __builtin_amdgcn_global_load_lds((gptr_t)(srcp[j] + k0), (lptr_t)(lbase + buf * STAGE + dstoff[j]), 16, 0, 0);
+    for (int j = 0; j < QW; ++j) issue1(j, s, buf);
   };
 
   // ---- per-lane fragment offsets (row r, k chunk c = 2 kk + (lane >> 5))
@@ -138,7 +154,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
       for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(b[p][j]));
     }
   };
-  auto mfmas = [&](const u32x4_t (&a)[3][MI], const u32x4_t (&b)[3][NJ]) {
+  // between(t) runs after the six MFMAs of accumulator tile t (ILV: the next stage's DMA pieces)
+  auto mfmas = [&](const u32x4_t (&a)[3][MI], const u32x4_t (&b)[3][NJ], auto&& between) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -150,80 +167,211 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[1][i]), bf(b[0][j]), c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[1][j]), c, 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf(a[0][i]), bf(b[0][j]), c, 0, 0, 0);
+        between(i * NJ + j);
       }
   };
   // one stage: k-slice 1's fragment reads are issued before k-slice 0's MFMAs (the scheduling
-  // barrier keeps them there), so their LDS latency hides under those MFMAs
-  auto compute = [&](int buf) {
+  // barrier keeps them there), so their LDS latency hides under those MFMAs.  ILV: the DMA
+  // pieces of stage s + 1 (into the other buffer, free since every wave passed this step's
+  // barrier) go out in the gaps after the first IT MFMA tiles — early, so they land before
+  // the next step's wait, and beside MFMAs, so no phase of the step issues DMA alone
+  constexpr int IT = MI * NJ < 3 ? MI * NJ : 3;  // tiles whose gaps carry the DMA pieces
+  auto compute = [&](int buf, int snext) {
     const uint32_t sb = l0 + buf * STAGE;
+    auto between = [&](int kk, int t) {
+      if constexpr (ILV) {
+        if (kk == 0 && t < IT) {
+          if (snext >= 0) {
+#pragma unroll
+            for (int j = t * QW / IT; j < (t + 1) * QW / IT; ++j) issue1(j, snext, buf ^ 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
     u32x4_t a0[3][MI], b0[3][NJ], a1[3][MI], b1[3][NJ];
+    X3P_T(t1);
     read_frags(sb, 0, a0, b0);
     land_frags(a0, b0);
+    X3P_T(t2);
+#ifdef TTS_STAMPS
+    c_land += t2 - t1;
+#endif
     read_frags(sb, 1, a1, b1);
     __builtin_amdgcn_sched_barrier(0);
-    mfmas(a0, b0);
+    mfmas(a0, b0, [&](int t) { between(0, t); });
     __builtin_amdgcn_sched_barrier(0);
     land_frags(a1, b1);
-    mfmas(a1, b1);
+    mfmas(a1, b1, [&](int t) { between(1, t); });
+#ifdef TTS_STAMPS
+    X3P_T(t3);
+    c_mfma += t3 - t2;
+#endif
   };
 
-  // ---- two stages in flight; stage s is read after its DMA was counted in and every wave
-  // passed the barrier, refilled (stage s + 2) after the barrier that ends its reads
-  issue(0, 0);
-  if (nsteps > 1) issue(1, 1);
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");
-    compute(s & 1);
-    asm volatile("s_barrier" ::: "memory");
-    if (s + 2 < nsteps) issue(s + 2, s & 1);
+  if constexpr (ILV) {
+    // one stage in flight: stage s + 1 is issued while stage s is multiplied; one barrier per
+    // step (it also ends every wave's reads of the buffer the next issue overwrites)
+    issue(0, 0);
+    for (int s = 0; s < nsteps; ++s) {
+      X3P_T(t0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");
+#ifdef TTS_STAMPS
+      X3P_T(t0b);
+      c_wait += t0b - t0;
+#endif
+      compute(s & 1, s + 1 < nsteps ? s + 1 : -1);
+    }
+  } else {
+    // ---- two stages in flight; stage s is read after its DMA was counted in and every wave
+    // passed the barrier, refilled (stage s + 2) after the barrier that ends its reads
+    issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");
+      compute(s & 1, -1);
+      asm volatile("s_barrier" ::: "memory");
+      if (s + 2 < nsteps) issue(s + 2, s & 1);
+    }
   }
 
-  // ---- epilogue (as gemm_bx3_kernel): lane owns column (lane & 31); rows (r&3) + 8(r>>2) +
-  // 4(lane>>5).  The residual values of an accumulator's 16 rows are loaded together
-  // (clamped rows, unconditional) before any of them is used: one L2 round trip, not 16
+  X3P_T(t_epi);
   const bool has_bias = g.bias != nullptr, has_resid = g.resid != nullptr;
+  // ---- epilogue through LDS: each wave parks its WTM x WTN fp32 tile in LDS (the K loop's
+  // stages are free once every wave passed the barrier) and reads it back as 16-B row pieces, so
+  // a store instruction writes whole contiguous rows (1 KiB of C per wave instruction, 4 bf16 per
+  // lane and plane) instead of one column element per lane in two rows (the accumulator layout:
+  // 256 store instructions per wave and tile set; measured 17 % of the kernel, stamps build).
+  // Same arithmetic per element: acc + bias, act, resid + v, split
+  constexpr int WTM = TM / WM, WTN = TN / WN;
+  static_assert(NW * WTM * WTN * 4 <= 2 * STAGE, "the output tiles must fit the stage buffers");
+  const bool vec = ((g.N | g.ldc) & 3) == 0 && (((size_t)g.C | (size_t)g.resid) & 15) == 0 &&
+                   (((size_t)g.Cp | (size_t)(g.cp_plane * 2)) & 7) == 0;
+  if (vec) {
+    asm volatile("s_barrier" ::: "memory");  // (every wave's fragment reads completed: land_frags)
+    float* tile = (float*)smem + wave * (WTM * WTN);
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int n = n0 + wn * (TN / WN) + j * 32 + (lane & 31);
-    const int nc = min(n, g.N - 1);
-    const float bias = has_bias ? g.bias[nc] : 0.f;
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int mb = m0 + wm * (TM / WM) + i * 32 + 4 * (lane >> 5);
-      float rv[16];
-      if (has_resid) {
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) rv[r] = g.resid[(size_t)min(mb + (r & 3) + 8 * (r >> 2), g.M - 1) * g.ldc + nc];
+        for (int r = 0; r < 16; ++r)
+          tile[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * WTN + j * 32 + (lane & 31)] = acc[i][j][r];
+    constexpr int LPR = WTN / 4, RPI = 64 / LPR, IT = WTM / RPI;  // lanes per row, rows per instruction
+    const int cq = lane % LPR, rr = lane / LPR;
+    const int n = n0 + wn * WTN + 4 * cq;
+    const int nc = min(n, g.N - 4);
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (has_bias) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bias[q] = g.bias[nc + q];
+    }
+    const int mb = m0 + wm * WTM + rr;
+    float4 rv[IT];
+    if (has_resid) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it) rv[it] = *(const float4*)(g.resid + (size_t)min(mb + it * RPI, g.M - 1) * g.ldc + nc);
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int m = mb + it * RPI;
+      const float4 a4 = *(const float4*)(tile + (rr + it * RPI) * WTN + 4 * cq);
+      float v[4] = {a4.x, a4.y, a4.z, a4.w};
+      const float rq[4] = {rv[it].x, rv[it].y, rv[it].z, rv[it].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = v[q] + bias[q];
+        if (g.act == 1) v[q] = v[q] / (1.0f + expf(-v[q]));
+        if (has_resid) v[q] = rq[q] + v[q];
       }
+      if (m < g.M && n < g.N) {
+        const size_t o = (size_t)m * g.ldc + n;
+        if (g.C) *(float4*)(g.C + o) = make_float4(v[0], v[1], v[2], v[3]);
+        if (g.Cp) {  // the consumer GEMM's planes (the split every producer uses)
+          uint32_t hw[2], mw[2], lw[2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb + (r & 3) + 8 * (r >> 2);
-        float v = acc[i][j][r] + bias;
-        if (g.act == 1) v = v / (1.0f + expf(-v));
-        if (has_resid) v = rv[r] + v;
-        if (m < g.M && n < g.N) {
-          const size_t o = (size_t)m * g.ldc + n;
-          if (g.C) g.C[o] = v;
-          if (g.Cp) {  // the consumer GEMM's planes (the split every producer uses)
-            asm("" : "+v"(v));  // (no contraction into v - h: see store_planes)
-            const float h = rbf(v), rm = v - h, mm = rbf(rm);
-            g.Cp[o] = f2bf(h);
-            g.Cp[g.cp_plane + o] = f2bf(mm);
-            g.Cp[2 * g.cp_plane + o] = f2bf(rm - mm);
+          for (int q = 0; q < 4; q += 2) {
+            float x0 = v[q], x1 = v[q + 1];
+            asm("" : "+v"(x0), "+v"(x1));  // (no contraction into v - h: see store_planes)
+            const float h0 = rbf(x0), r0 = x0 - h0, m0v = rbf(r0);
+            const float h1 = rbf(x1), r1 = x1 - h1, m1v = rbf(r1);
+            hw[q >> 1] = (uint32_t)f2bf(h0) | ((uint32_t)f2bf(h1) << 16);
+            mw[q >> 1] = (uint32_t)f2bf(m0v) | ((uint32_t)f2bf(m1v) << 16);
+            lw[q >> 1] = (uint32_t)f2bf(r0 - m0v) | ((uint32_t)f2bf(r1 - m1v) << 16);
+          }
+          *(uint2*)(g.Cp + o) = make_uint2(hw[0], hw[1]);
+          *(uint2*)(g.Cp + g.cp_plane + o) = make_uint2(mw[0], mw[1]);
+          *(uint2*)(g.Cp + 2 * g.cp_plane + o) = make_uint2(lw[0], lw[1]);
+        }
+      }
+    }
+  } else {
+  // ---- fallback (unaligned or odd widths): lane owns column (lane & 31); rows (r&3) +
+  // 8(r>>2) + 4(lane>>5), as gemm_bx3_kernel; the residual values of an accumulator's 16 rows
+  // are loaded together before any of them is used
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * (TN / WN) + j * 32 + (lane & 31);
+      const int nc = min(n, g.N - 1);
+      const float bias = has_bias ? g.bias[nc] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int mb = m0 + wm * (TM / WM) + i * 32 + 4 * (lane >> 5);
+        float rv[16];
+        if (has_resid) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rv[r] = g.resid[(size_t)min(mb + (r & 3) + 8 * (r >> 2), g.M - 1) * g.ldc + nc];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mb + (r & 3) + 8 * (r >> 2);
+          float v = acc[i][j][r] + bias;
+          if (g.act == 1) v = v / (1.0f + expf(-v));
+          if (has_resid) v = rv[r] + v;
+          if (m < g.M && n < g.N) {
+            const size_t o = (size_t)m * g.ldc + n;
+            if (g.C) g.C[o] = v;
+            if (g.Cp) {  // the consumer GEMM's planes (the split every producer uses)
+              asm("" : "+v"(v));  // (no contraction into v - h: see store_planes)
+              const float h = rbf(v), rm = v - h, mm = rbf(rm);
+              g.Cp[o] = f2bf(h);
+              g.Cp[g.cp_plane + o] = f2bf(mm);
+              g.Cp[2 * g.cp_plane + o] = f2bf(rm - mm);
+            }
           }
         }
       }
     }
   }
+#ifdef TTS_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  X3P_T(t_end);
+  if (lane == 0) {
+    atomicAdd(&g_x3p_cyc[0], c_wait);
+    atomicAdd(&g_x3p_cyc[1], c_land);
+    atomicAdd(&g_x3p_cyc[2], c_mfma);
+    atomicAdd(&g_x3p_cyc[3], t_end - t_epi);
+    atomicAdd(&g_x3p_cyc[4], t_end - t_entry);
+    atomicAdd(&g_x3p_cyc[5], 1ull);
+  }
+#endif
 }
 
 template <int TM, int TN, int WM, int WN>
 static void launch_x3p(const GemmF32Args& g, hipStream_t s) {
   constexpr size_t lds = 2 * 3 * (size_t)(TM + TN) * 64;
   const int tiles = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
-  hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  // the one-stage-ahead schedule with the DMA between the MFMAs on the 8- and 4-wave 64x64-per-
+  // wave tiles (a step is long enough to cover the DMA's latency); the two-stage schedule on
+  // the small tiles, whose steps are not (one 650-code utterance 4.8 -> 5.3 ms with the first,
+  // profiles/r5h_ab_codec_ilv.txt).  TTS_CODEC_X3P_ILV=0 / 1 forces one (A/B)
+  static const int ilv_env = getenv("TTS_CODEC_X3P_ILV") ? atoi(getenv("TTS_CODEC_X3P_ILV")) : -1;
+  const bool ilv = ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64);
+  if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  else hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
 }
 
 bool gemm_x3p_supported(const GemmF32Args& g) {
@@ -249,6 +397,20 @@ void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s) {
     case 3: launch_x3p<64, 64, 2, 2>(g, s); break;
     default: launch_x3p<32, 32, 1, 1>(g, s); break;  // one wave: a lone utterance's small GEMMs
   }
+}
+
+void x3p_stamps_dump(FILE* f) {
+#ifdef TTS_STAMPS
+  unsigned long long h[8] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_x3p_cyc), sizeof(h)) != hipSuccess) return;
+  const double tot = (double)(h[4] ? h[4] : 1);
+  fprintf(f, "x3p phases over %llu waves: wait+barrier %.3f  kk0 landing %.3f  MFMA phase %.3f  epilogue %.3f  "
+             "(of %.0f cycles per wave)\n", h[5], h[0] / tot, h[1] / tot, h[2] / tot, h[3] / tot, tot / (h[5] ? h[5] : 1));
+  const unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_x3p_cyc), z, sizeof(z));
+#else
+  (void)f;
+#endif
 }
 
 }  // namespace tts

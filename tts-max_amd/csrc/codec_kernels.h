@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdio>
 
 namespace tts {
 
@@ -44,6 +45,8 @@ void launch_gemm_f32(const GemmF32Args& g, hipStream_t s);
 // the same contraction with A and B both given as planes (Ap, Bp; codec_gemm.hip)
 bool gemm_x3p_supported(const GemmF32Args& g);
 void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s);
+// diagnostic (stamps) build: print and reset the K-loop phase sums of gemm_x3p; no-op otherwise
+void x3p_stamps_dump(FILE* f);
 // planes[0..3n) = the (h, m, l) bf16 split of x[0..n) the GEMM applies to its operands
 void launch_split_planes(const float* x, uint16_t* planes, long long n, hipStream_t s);
 

@@ -14,8 +14,6 @@
 // the A-operand layouts of S^T = K.Q^T and O^T = V^T.P^T on v_mfma_f32_16x16x32_bf16, so the
 // kernels load every fragment straight into registers.  Both kernels write the attention
 // output (bf16, [rows][H*D]) directly: no chunk partials, no merge pass.
-#include <stdexcept>
-
 #include "hip_common.h"
 #include "lm_kernels.h"
 #include "lm_attn_core.h"
@@ -72,58 +70,52 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
   const bf16_t* vtc = a.vtcache + kvbase;
   unsigned long long* stp = a.stamps ? a.stamps + 16384 + (size_t)blockIdx.x * 8 : nullptr;
   TTS_STAMP(stp, 0);
-  // This thread's q | k | v element (i = tid < G*D + 2D: the group's q heads, the new k, the
-  // new v) and the RoPE cos / sin of its dimension, loaded FIRST: loads retire in issue order,
-  // so behind the K / V^T fragments they would land only after the whole first pass had (the
-  // attention waited ~4 us for 1.5 KB of q|k|v at 32 rows, profiles/r4i_stamps_tts1_32.txt).
-  // The element is the K-sliced QKV launch's four fp32 slice partials (a.qkv_part, summed in
-  // slice order) or the bf16 qkv row's 32-bit word that holds it.  Every load is unconditional
-  // with a fixed count (4 words, cos, sin, then the fragments; positions past ctx clamped), so
-  // the compiler's vmcnt waits stay exact and the sums wait for their own loads only
-  static_assert(DEC_G * D + 2 * D <= NW * 64, "one q|k|v element per thread");
-  constexpr int NSL = 4;  // (host: qkv_nsl == 4 whenever qkv_part is set)
-  constexpr int H2 = D / 2;
-  const bool has_part = a.qkv_part != nullptr;
-  const int ei = min(tid, DEC_G * D + 2 * D - 1);
-  const int col = ei < DEC_G * D ? kvh * DEC_G * D + ei
-                : (ei < DEC_G * D + D ? a.H * D + kvh * D + ei - DEC_G * D
-                                      : a.H * D + a.KVH * D + kvh * D + ei - DEC_G * D - D);
-  const int rd = ei < DEC_G * D ? ei % D : (ei - DEC_G * D) % D;  // the element's dimension
-  uint32_t pw[NSL];
-  {
-    const uint32_t* src = has_part ? (const uint32_t*)a.qkv_part : (const uint32_t*)(a.qkv + (size_t)row * a.ld_qkv);
-#pragma unroll
-    for (int sl = 0; sl < NSL; ++sl)
-      pw[sl] = src[has_part ? ((size_t)sl * a.rows + row) * a.ld_qkv + col : (size_t)(col >> 1)];
-  }
-  const float rcos = bf2f(a.rope_cos[(size_t)pos * D + rd]), rsin = bf2f(a.rope_sin[(size_t)pos * D + rd]);
-  __builtin_amdgcn_sched_barrier(0);  // (keep the fragment loads behind these)
-  // this wave's first-pass fragments (waves past ctx load clamped positions, never used)
+  // this wave's first-pass fragments before anything else (vmcnt retires in issue order).
+  // Head dim 64 addresses them with 32-bit offsets (the 64-bit ones spilled across the later
+  // passes); at 128 the 64-bit form allocates without spills.  (Loading q|k|v and the RoPE
+  // terms ahead of the fragments was measured slower again in round 5: 32 rows 10.1 -> 12.5 us,
+  // profiles/r5h_ab_32.txt)
   u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
-  dec_load_k<D, PW, true>(kc, min(wave * PW, ctx - 1), ctx, lane, kf);
-  dec_load_v<D, PW, true>(vtc, a.max_seq, wave * PW, lane, vf);
-  // the group's q | k | v in LDS (bf16), then RoPE of the q heads and of the new k (HF
-  // apply_rotary_pos_emb in bf16) from there
-  __shared__ __attribute__((aligned(16))) bf16_t raw[DEC_G * D + 2 * D];
-  if (tid < DEC_G * D + 2 * D) {
-    raw[tid] = has_part ? f2bf((((0.f + __uint_as_float(pw[0])) + __uint_as_float(pw[1])) + __uint_as_float(pw[2])) +
-                               __uint_as_float(pw[3]))  // slice order, from +0
-                        : (bf16_t)((col & 1) ? (pw[0] >> 16) : (pw[0] & 0xffffu));
+  if (wave * PW < ctx) {
+    dec_load_k<D, PW, D == 64>(kc, wave * PW, ctx, lane, kf);
+    dec_load_v<D, PW, D == 64>(vtc, a.max_seq, wave * PW, lane, vf);
   }
-  lds_barrier();
-  if (tid < DEC_G * D + D) {
-    const bf16_t* base = raw + (tid < DEC_G * D ? (tid / D) * D : DEC_G * D);
-    const float r = rope_elem(base[rd], base[rd < H2 ? rd + H2 : rd - H2], rd < H2, rcos, rsin);
-    if (tid < DEC_G * D) {
-      qs[tid] = r;
+  // RoPE of the group's q heads and of the new k (HF apply_rotary_pos_emb in bf16)
+  const bf16_t* qrow = a.qkv + (size_t)row * a.ld_qkv;
+  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
+  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
+  // the group's q | k | v: columns of the qkv row, or sums of a K-sliced launch's partials
+  __shared__ __attribute__((aligned(16))) bf16_t raw[DEC_G * D + 2 * D];
+  const bf16_t* qsrc = qrow + kvh * DEC_G * D;
+  const bf16_t* ksrc = qrow + a.H * D + kvh * D;
+  const bf16_t* vsrc = qrow + a.H * D + a.KVH * D + kvh * D;
+  if (a.qkv_part) {
+    for (int i = tid; i < DEC_G * D + 2 * D; i += NW * 64) {
+      const int col = i < DEC_G * D ? kvh * DEC_G * D + i
+                    : (i < DEC_G * D + D ? a.H * D + kvh * D + i - DEC_G * D
+                                         : a.H * D + a.KVH * D + kvh * D + i - DEC_G * D - D);
+      float v = 0.f;
+      for (int sl = 0; sl < a.qkv_nsl; ++sl) v += a.qkv_part[((size_t)sl * a.rows + row) * a.ld_qkv + col];
+      raw[i] = f2bf(v);
+    }
+    lds_barrier();
+    qsrc = raw;
+    ksrc = raw + DEC_G * D;
+    vsrc = raw + DEC_G * D + D;
+  }
+  for (int i = tid; i < DEC_G * D + D; i += NW * 64) {
+    if (i < DEC_G * D) {
+      const int g = i / D, d = i % D;
+      qs[i] = rope_at<D>(qsrc + g * D, d, cosr, sinr);
     } else {
-      knew[rd] = f2bf(r);
-      vnew[rd] = raw[DEC_G * D + D + rd];
+      const int d = i - DEC_G * D;
+      knew[d] = f2bf(rope_at<D>(ksrc, d, cosr, sinr));
+      vnew[d] = vsrc[d];
     }
   }
   lds_barrier();
   TTS_STAMP(stp, 2);
-  dec_attend<D, PW, NW, true>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
+  dec_attend<D, PW, NW, D == 64>(kc, vtc, a.max_seq, ctx, a.scale, qs, knew, vnew, red, kf, vf,
                               a.out + (size_t)row * a.H * D + kvh * DEC_G * D);
   TTS_STAMP(stp, 3);
   // the new position into the cache, after this workgroup's reads (no other workgroup reads
@@ -224,7 +216,6 @@ void launch_attn_decode_step(const AttnArgs& a, hipStream_t s) {
     return;
   }
   const dim3 grid(a.rows * a.KVH);
-  if (a.qkv_part && a.qkv_nsl != 4) throw std::runtime_error("decode attention: K-sliced q|k|v must have 4 slices");
   if (a.D == 64) hipLaunchKernelGGL((attn_decode_kernel<64>), grid, dim3(dec_nw<64>() * 64), 0, s, a);
   else hipLaunchKernelGGL((attn_decode_kernel<128>), grid, dim3(dec_nw<128>() * 64), 0, s, a);
 }

@@ -24,8 +24,6 @@ __host__ __device__ inline int wgemm_red_floats(int waves, int ksplit, int ng, i
   const int segs = (M * (Kl / 8) + 63) / 64;
   r = r > segs ? r : segs;
   r = r > Kl / 2 ? r : Kl / 2;  // RMSNorm weight (bf16) parked here during the LDS-DMA prologue
-  const int wsg = Kl / 2 + M * (Kl / 512);  // ... followed by the [M][K / 512] segment sums
-  r = r > wsg ? r : wsg;
   return r + 64;
 }
 
@@ -584,42 +582,75 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
     TTS_STAMP(stp, 6);  // (A rows landed)
     if (a.diag & kWgemmDiagMask & 16) {
     } else if constexpr (NORM) {
-      // RMSNorm of the landed rows, spread over every wave (a wave per row left half the
-      // waves idle and made each busy one scale a whole row: ~4 us at 8 rows of 4096):
-      // (a) the canonical segment sums (chunk_sumsq + the wave DPP tree over each 512-value
-      //     segment: the same bits as every other RMSNorm path) of all (row, segment) pairs;
-      // (b) each wave scales only the A columns it will read (its k-part's k-tiles) of every
-      //     row, the UPW waves sharing a k-part splitting them; r from the segments in order
-      const bf16_t* gw = (const bf16_t*)red;      // (the parked RMSNorm weight)
-      float* segs = red + (a.K >> 1);              // [M][K / 512] segment sums
-      const int nseg = a.K >> 9;
-      for (int p = wave; p < M * nseg; p += WAVES) {
-        const int m = p / nseg, sg = p - m * nseg;
-        const float sv = wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xs + (size_t)m * ldxs + sg * 512 + lane * 8)));
-        if (lane == 0) segs[p] = sv;
-      }
-      __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
-      __builtin_amdgcn_s_barrier();
-      // r of row m in lane m (M <= 64), read back uniformly (s_readlane) per row below
-      float rv = 0.f;
-      if (lane < M) {
-        float ss = 0.f;
-        for (int sg = 0; sg < nseg; ++sg) ss += segs[lane * nseg + sg];  // (segments in order)
-        rv = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-      }
-      const int Q = kc * kt_pc * 4;  // (k-tile, 8-column chunk) items of this k-part (non-sliced: kpart == kq)
-      for (int x = ugrp * 64 + lane; x < Q; x += UPW * 64) {
-        const int t = x >> 2, ch = t / kt_pc;
-        const int k = (ch * KTc + kq * kt_pc + (t - ch * kt_pc)) * 32 + (x & 3) * 8;
-        const u32x4_t g = *(const u32x4_t*)(gw + k);
-        for (int m = 0; m < M; ++m) {
-          const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), m));
-          bf16_t* xr = xs + (size_t)m * ldxs + k;
-          u32x4_t v = *(const u32x4_t*)xr;
+      // RMSNorm of the landed rows, a wave per row (canonical order: chunk_sumsq + the wave
+      // DPP tree per 512-value segment, segments in order).  Spreading the segment sums and the
+      // scaling over every wave gave the same bits and was slower (round 5: TTS-1 8 rows qkv
+      // 6.9 -> 9.8 us, profiles/r5h_ab_8.txt; round 4's four rewrites: neutral).
+      // Four segments per batch: their LDS reads are issued together and their four DPP trees
+      // interleave (one segment at a time was a chain of LDS-read latency + six dependent DPP
+      // steps per 512 values); same sums, same order
+      const bf16_t* gw = (const bf16_t*)red;
+      // (one at a time where the weight ring's registers leave no room: the 2..16-row TTS-1
+      // fused launch spilled with the batches)
+      constexpr bool BATCH = !(FATT && KU < 4);
+      if constexpr (!BATCH) {
+        for (int m = wave; m < M; m += WAVES) {
+          bf16_t* xr = xs + (size_t)m * ldxs;
+          float ss = 0.f;
+          for (int k0 = 0; k0 < a.K; k0 += 512)  // canonical order (chunk_sumsq)
+            ss += wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xr + k0 + lane * 8)));
+          const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+          for (int k = lane * 8; k < a.K; k += 512) {
+            u32x4_t v = *(const u32x4_t*)(xr + k);
+            const u32x4_t g = *(const u32x4_t*)(gw + k);
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
-          *(u32x4_t*)xr = v;
+            for (int q = 0; q < 4; ++q)
+              v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+            *(u32x4_t*)(xr + k) = v;
+          }
+        }
+      } else {
+        constexpr int NB = 4, SB = 2;
+        const int k4 = a.K & ~(512 * NB - 1);
+        for (int m = wave; m < M; m += WAVES) {
+          bf16_t* xr = xs + (size_t)m * ldxs;
+          float ss = 0.f;
+          for (int k0 = 0; k0 < k4; k0 += 512 * NB) {  // canonical order (chunk_sumsq, segments in order)
+            u32x4_t v[NB];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) v[q] = *(const u32x4_t*)(xr + k0 + q * 512 + lane * 8);
+            float sv[NB];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) sv[q] = wave_sum_dpp(chunk_sumsq(v[q]));
+#pragma unroll
+            for (int q = 0; q < NB; ++q) ss += sv[q];
+          }
+          for (int k0 = k4; k0 < a.K; k0 += 512) ss += wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xr + k0 + lane * 8)));
+          const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+          auto scale = [&](u32x4_t& v, const u32x4_t& g) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+          };
+          const int ks = a.K & ~(512 * SB - 1);
+          for (int k0 = 0; k0 < ks; k0 += 512 * SB) {  // (SB at a time: the ring's registers are live)
+            u32x4_t v[SB], g[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+              v[q] = *(const u32x4_t*)(xr + k0 + q * 512 + lane * 8);
+              g[q] = *(const u32x4_t*)(gw + k0 + q * 512 + lane * 8);
+            }
+#pragma unroll
+            for (int q = 0; q < SB; ++q) {
+              scale(v[q], g[q]);
+              *(u32x4_t*)(xr + k0 + q * 512 + lane * 8) = v[q];
+            }
+          }
+          for (int k = ks + lane * 8; k < a.K; k += 512) {
+            u32x4_t v = *(const u32x4_t*)(xr + k);
+            scale(v, *(const u32x4_t*)(gw + k));
+            *(u32x4_t*)(xr + k) = v;
+          }
         }
       }
       __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
