@@ -49,7 +49,7 @@ TTS_DEV u32x4_t lds_rd16(uint32_t addr) {
   return v;
 }
 
-template <int TM, int TN, int WM, int WN, bool ILV>
+template <int TM, int TN, int WM, int WN, bool ILV, int NS = 2>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int MI = TM / WM / 32, NJ = TN / WN / 32;  // 32x32 accumulators per wave
@@ -176,14 +176,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   // barrier) go out in the gaps after the first IT MFMA tiles — early, so they land before
   // the next step's wait, and beside MFMAs, so no phase of the step issues DMA alone
   constexpr int IT = MI * NJ < 3 ? MI * NJ : 3;  // tiles whose gaps carry the DMA pieces
-  auto compute = [&](int buf, int snext) {
+  auto compute = [&](int buf, int snext, int nbuf) {
     const uint32_t sb = l0 + buf * STAGE;
     auto between = [&](int kk, int t) {
       if constexpr (ILV) {
         if (kk == 0 && t < IT) {
           if (snext >= 0) {
 #pragma unroll
-            for (int j = t * QW / IT; j < (t + 1) * QW / IT; ++j) issue1(j, snext, buf ^ 1);
+            for (int j = t * QW / IT; j < (t + 1) * QW / IT; ++j) issue1(j, snext, nbuf);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -210,18 +210,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   };
 
   if constexpr (ILV) {
-    // one stage in flight: stage s + 1 is issued while stage s is multiplied; one barrier per
-    // step (it also ends every wave's reads of the buffer the next issue overwrites)
-    issue(0, 0);
+    // NS - 1 stages in flight: stage s + NS - 1 is issued while stage s is multiplied, into the
+    // buffer stage s - 1 used (every wave left it: this step's barrier); one barrier per step
+    static_assert(NS == 2 || NS == 3, "two or three stage buffers");
+    constexpr int AHEAD = (NS - 2) * QW;  // pieces of the younger stages allowed in flight
+#pragma unroll
+    for (int q = 0; q < NS - 1; ++q)
+      if (q < nsteps) issue(q, q);
+    int buf = 0;
     for (int s = 0; s < nsteps; ++s) {
       X3P_T(t0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (s + NS - 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AHEAD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_barrier" ::: "memory");
 #ifdef TTS_STAMPS
       X3P_T(t0b);
       c_wait += t0b - t0;
 #endif
-      compute(s & 1, s + 1 < nsteps ? s + 1 : -1);
+      const int nbuf = buf == 0 ? NS - 1 : buf - 1;
+      compute(buf, s + NS - 1 < nsteps ? s + NS - 1 : -1, nbuf);
+      buf = buf == NS - 1 ? 0 : buf + 1;
     }
   } else {
     // ---- two stages in flight; stage s is read after its DMA was counted in and every wave
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
       if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_barrier" ::: "memory");
-      compute(s & 1, -1);
+      compute(s & 1, -1, 0);
       asm volatile("s_barrier" ::: "memory");
       if (s + 2 < nsteps) issue(s + 2, s & 1);
     }
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   // 256 store instructions per wave and tile set; measured 17 % of the kernel, stamps build).
   // Same arithmetic per element: acc + bias, act, resid + v, split
   constexpr int WTM = TM / WM, WTN = TN / WN;
-  static_assert(NW * WTM * WTN * 4 <= 2 * STAGE, "the output tiles must fit the stage buffers");
+  static_assert(NW * WTM * WTN * 4 <= NS * STAGE, "the output tiles must fit the stage buffers");
   const bool vec = ((g.N | g.ldc) & 3) == 0 && (((size_t)g.C | (size_t)g.resid) & 15) == 0 &&
                    (((size_t)g.Cp | (size_t)(g.cp_plane * 2)) & 7) == 0;
   if (vec) {
@@ -360,17 +368,18 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
 #endif
 }
 
-template <int TM, int TN, int WM, int WN>
+template <int TM, int TN, int WM, int WN, int NS = 2>
 static void launch_x3p(const GemmF32Args& g, hipStream_t s) {
-  constexpr size_t lds = 2 * 3 * (size_t)(TM + TN) * 64;
+  constexpr size_t lds = NS * 3 * (size_t)(TM + TN) * 64;
+  static_assert(lds <= 160 * 1024, "LDS");
   const int tiles = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
   // the one-stage-ahead schedule with the DMA between the MFMAs on the 8- and 4-wave 64x64-per-
   // wave tiles (a step is long enough to cover the DMA's latency); the two-stage schedule on
   // the small tiles, whose steps are not (one 650-code utterance 4.8 -> 5.3 ms with the first,
   // profiles/r5h_ab_codec_ilv.txt).  TTS_CODEC_X3P_ILV=0 / 1 forces one (A/B)
   static const int ilv_env = getenv("TTS_CODEC_X3P_ILV") ? atoi(getenv("TTS_CODEC_X3P_ILV")) : -1;
-  const bool ilv = ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64);
-  if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  const bool ilv = NS == 3 || (ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64));
+  if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
   else hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
 }
 
@@ -395,6 +404,7 @@ void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s) {
     case 1: launch_x3p<128, 128, 2, 2>(g, s); break;
     case 2: launch_x3p<128, 64, 2, 2>(g, s); break;
     case 3: launch_x3p<64, 64, 2, 2>(g, s); break;
+    case 5: launch_x3p<128, 128, 2, 4, 3>(g, s); break;  // (8 waves of 64x32, three stages: experiment)
     default: launch_x3p<32, 32, 1, 1>(g, s); break;  // one wave: a lone utterance's small GEMMs
   }
 }

@@ -642,7 +642,9 @@ void launch_layernorm_f32(const float* x, int T, int C, const float* w, const fl
 // LDS tile to re-read it as the A operand, and accumulates O += P V.
 constexpr int AB = 64;        // queries per workgroup / keys per chunk
 constexpr int AD = 64;        // head dim
-constexpr int APL = AB + 8;   // bf16 row stride of the K / V^T planes (144 B: conflict-free b128 reads)
+constexpr int APL = AB + 8;   // bf16 row stride of the K / V^T planes (144 B; 160 B, conflict-free in
+                              // ds_read_b128's lane groups, took the conflicts from 43 % to 32 % of
+                              // the LDS cycles and changed nothing else: profiles/r5l_*)
 constexpr int APS = AB + 4;   // fp32 row stride of a wave's P tile
 constexpr size_t attn_lds(int nw) { return 2 * 3 * 64 * APL * 2 + (size_t)nw * 16 * APS * 4; }
 
@@ -904,11 +906,8 @@ __global__ __launch_bounds__(64 * NW) void codec_attn_kernel(const float* __rest
   }
 }
 
-// queries per workgroup: 64 (4 waves) or 128 (8 waves: TTS_CODEC_ATTN_W=8)
-static int attn_waves() {
-  static const int w = (getenv("TTS_CODEC_ATTN_W") && atoi(getenv("TTS_CODEC_ATTN_W")) == 8) ? 8 : 4;
-  return w;
-}
+// queries per workgroup: 64 (4 waves; the 8-wave form was dropped in round 5)
+static int attn_waves() { return 4; }
 int codec_attn_qrows() { return 16 * attn_waves(); }
 int codec_attn_qblocks(int T) { return (T + codec_attn_qrows() - 1) / codec_attn_qrows(); }
 
@@ -920,12 +919,8 @@ void launch_codec_attention(const float* qkv, const CodecSeg* seg, const int2* q
   // either way, profiles/r4e_ab_codec_expf.txt: the softmax is not what bounds this kernel), so
   // the reference's exp stays.  TTS_CODEC_EXPF=0: v_exp_f32
   static const int expf_mode = getenv("TTS_CODEC_EXPF") ? atoi(getenv("TTS_CODEC_EXPF")) : 1;
-  if (attn_waves() == 8)
-    hipLaunchKernelGGL(codec_attn_kernel<8>, grid, dim3(512), attn_lds(8), s, qkv, seg, qblk, heads,
-                       (const float2*)rope_cs, out, expf_mode, outp, plane);
-  else
-    hipLaunchKernelGGL(codec_attn_kernel<4>, grid, dim3(256), attn_lds(4), s, qkv, seg, qblk, heads,
-                       (const float2*)rope_cs, out, expf_mode, outp, plane);
+  hipLaunchKernelGGL(codec_attn_kernel<4>, grid, dim3(256), attn_lds(4), s, qkv, seg, qblk, heads,
+                     (const float2*)rope_cs, out, expf_mode, outp, plane);
 }
 
 // (cos, sin) of the torchtune rotation for every (head h, pair p): angle h * 10000^(-2p/64),
