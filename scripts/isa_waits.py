@@ -33,7 +33,7 @@ def analyse(body):
     dma = next((k for k, l in enumerate(t) if l.startswith("global_load_lds")), None)
     if dma is None:
         return res
-    nt = next((k for k in range(dma, len(t)) if t[k].startswith("global_load_dwordx4") and t[k].endswith(" nt")), None)
+    nt = next((k for k in range(dma, len(t)) if t[k].startswith(("global_load_dwordx4", "buffer_load_dwordx4")) and t[k].endswith(" nt")), None)
     if nt is None:
         return res
     res["pre_stream"] = sum(1 for k in range(dma, nt) if t[k].startswith("s_waitcnt vmcnt(0)"))
