@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 5, session q: the RMSNorm prologue's scaling spread over every wave by column block
+# (wave-per-row statistic kept); GPU suite, LM A/B against session i's library (ids md5 must
+# match) at 8 / 16 rows and the TTS-1-Max shard, and the stamps of the new prologue
+set -u
+O=gpurun_out
+T=${1:-r5q}
+mkdir -p $O
+export TMPDIR=/tmp
+bash scripts/gpu_round.sh $T tests || exit $?
+export AB_V0=$PWD/ablib/lib_r5i.so AB_V1=$PWD/tts-max_amd/tts_amd/libtts_mi355x.so
+AB_ARCH=tts1-max timeout -k 10 500 python scripts/env_ab_probe.py TTS_LIB_PATH 8 2 > $O/${T}_ab_max8.txt 2>&1 || exit $?
+cat $O/${T}_ab_max8.txt
+timeout -k 10 300 python scripts/env_ab_probe.py TTS_LIB_PATH 8 2 > $O/${T}_ab_8.txt 2>&1 || exit $?
+cat $O/${T}_ab_8.txt
+timeout -k 10 300 python scripts/env_ab_probe.py TTS_LIB_PATH 16 1 > $O/${T}_ab_16.txt 2>&1 || exit $?
+cat $O/${T}_ab_16.txt
+unset AB_V0 AB_V1
+timeout -k 10 300 python scripts/stamp_probe.py 452 8 tts1-max 2>&1 | grep -v amdgpu.ids > $O/${T}_stamps_max8.txt
+rc=$?
+head -16 $O/${T}_stamps_max8.txt
+exit $rc

@@ -68,6 +68,8 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn
         print(f"  entry {q(us[:, 0])}  prologue {q(us[:, 1])}  streamed {q(us[:, 2])}  epilogue {q(us[:, 3])}")
         if not np.all(np.isnan(us[:, 6])):
             print(f"  A rows landed (LDS-DMA) {q(us[:, 6])}")
+        if not np.all(np.isnan(us[:, 7])):
+            print(f"  RMSNorm (wave 0): row statistic {q(us[:, 7])}  rows scaled {q(us[:, 24])}")
 
         w = us[:, 8:24]
         print(f"  waves streamed: first {q(np.nanmin(w, 1))} last {q(np.nanmax(w, 1))}  split-K barrier {q(us[:, 4])}  summed {q(us[:, 5])}")

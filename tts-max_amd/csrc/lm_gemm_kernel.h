@@ -627,6 +627,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           }
           for (int k0 = k4; k0 < a.K; k0 += 512) ss += wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xr + k0 + lane * 8)));
           const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+          if (m == 0) TTS_STAMP(stp, 7);  // (wave 0: row 0's statistic)
           auto scale = [&](u32x4_t& v, const u32x4_t& g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -653,6 +654,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           }
         }
       }
+      TTS_STAMP(stp, 24);  // (wave 0: its rows normalised, before the barrier)
       __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
       __builtin_amdgcn_s_barrier();
     }
