@@ -215,3 +215,44 @@ def test_ragged_batch_in_several_passes_and_two_upsample_stages():
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(res["codec-48k"]) and all(res["codec-24k-d2"]), res
+
+
+_SCHED_CHILD = r'''
+import hashlib, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "tts-max_amd"))
+from tts_amd import configs
+from tts_amd.codec import MI355XAudioDecoder
+dec = MI355XAudioDecoder.synthetic(configs.CODEC_ARCHS["codec-24k"], seed=0xC0DEC, max_codes=1024)
+rng = np.random.default_rng(5)
+utts = [rng.integers(0, 65536, size=int(n)).tolist() for n in [650, 13, 400, 1, 257, 650, 96, 511]]
+wav = dec.decode_batch(utts)
+print(hashlib.md5(np.concatenate(wav).tobytes()).hexdigest())
+'''
+
+
+def _sched_md5(env):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _SCHED_CHILD, root], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout.strip().splitlines()[-1]
+
+
+@pytest.fixture(scope="module")
+def sched_default_md5():
+    return _sched_md5({})
+
+
+@pytest.mark.parametrize("env", [{"TTS_CODEC_X3P": "0"}, {"TTS_CODEC_X3P_ILV": "0"}, {"TTS_CODEC_X3P_ILV": "1"},
+                                 {"TTS_CODEC_X3P_TILE": "5"}, {"TTS_CODEC_X3P_TILE": "4"},
+                                 {"TTS_CODEC_X3P_PP": "1"}],
+                         ids=["bx3", "ilv0", "ilv1", "tile5_3stage", "tile4_1wave", "pp"])
+def test_codec_gemm_schedules_same_bits(env, sched_default_md5):
+    """Every codec GEMM form — the fp32-staging kernel, the planes kernel on each tile shape and
+    DMA schedule — sweeps an output's K in the same order, so a ragged batch decodes to the
+    same bits under each (each form in its own process: the switches are read once)."""
+    assert _sched_md5(env) == sched_default_md5, env

@@ -49,7 +49,7 @@ TTS_DEV u32x4_t lds_rd16(uint32_t addr) {
   return v;
 }
 
-template <int TM, int TN, int WM, int WN, bool ILV, int NS = 2>
+template <int TM, int TN, int WM, int WN, bool ILV, int NS = 2, bool PP = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int MI = TM / WM / 32, NJ = TN / WN / 32;  // 32x32 accumulators per wave
@@ -76,13 +76,21 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   const int nsteps = g.K / 32;
 
   // ---- per-lane DMA sources: row (lane >> 2) of each 16-row block, chunk (lane & 3) ^ swizzle
+  // PP: only the upper half of the waves (one per SIMD) issue the DMA, twice the pieces each,
+  // between their first MFMA tiles; the lower half starts its MFMAs right after the barrier, so
+  // the two waves of a SIMD run out of phase and one of them is multiplying while the other
+  // issues or lands fragments
+  constexpr int QD = PP ? 2 * QW : QW;        // pieces per issuing wave
+  constexpr int NL = PP ? NW / 2 : NW;        // issuing waves
+  const bool loader = !PP || wave >= NW - NL;
+  const int lw = PP ? wave - (NW - NL) : wave;
   const int drow = lane >> 2;
   const int dchunk = (lane & 3) ^ ((lane >> 4) & 3);
-  const uint16_t* srcp[QW];
-  uint32_t dstoff[QW];
+  const uint16_t* srcp[QD];
+  uint32_t dstoff[QD];
 #pragma unroll
-  for (int j = 0; j < QW; ++j) {
-    const int q = wave + j * NW;
+  for (int j = 0; j < QD; ++j) {
+    const int q = min(max(lw, 0) + j * NL, QA + QB - 1);
     if (q < QA) {
       const int p = q / (TM / 16), rb = q % (TM / 16);
       const int r = min(m0 + rb * 16 + drow, g.M - 1);
@@ -100,8 +108,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
     __builtin_amdgcn_global_load_lds((gptr_t)(srcp[j] + s * 32), (lptr_t)(lbase + buf * STAGE + dstoff[j]), 16, 0, 0);
   };
   auto issue = [&](int s, int buf) {
+    if (loader) {
 #pragma unroll
-    for (int j = 0; j < QW; ++j) issue1(j, s, buf);
+      for (int j = 0; j < QD; ++j) issue1(j, s, buf);
+    }
   };
 
   // ---- per-lane fragment offsets (row r, k chunk c = 2 kk + (lane >> 5))
@@ -181,9 +191,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
     auto between = [&](int kk, int t) {
       if constexpr (ILV) {
         if (kk == 0 && t < IT) {
-          if (snext >= 0) {
+          if (snext >= 0 && loader) {
 #pragma unroll
-            for (int j = t * QW / IT; j < (t + 1) * QW / IT; ++j) issue1(j, snext, nbuf);
+            for (int j = t * QD / IT; j < (t + 1) * QD / IT; ++j) issue1(j, snext, nbuf);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -213,7 +223,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
     // NS - 1 stages in flight: stage s + NS - 1 is issued while stage s is multiplied, into the
     // buffer stage s - 1 used (every wave left it: this step's barrier); one barrier per step
     static_assert(NS == 2 || NS == 3, "two or three stage buffers");
-    constexpr int AHEAD = (NS - 2) * QW;  // pieces of the younger stages allowed in flight
+    constexpr int AHEAD = (NS - 2) * QD;  // pieces of the younger stages allowed in flight
 #pragma unroll
     for (int q = 0; q < NS - 1; ++q)
       if (q < nsteps) issue(q, q);
@@ -379,7 +389,11 @@ static void launch_x3p(const GemmF32Args& g, hipStream_t s) {
   // profiles/r5h_ab_codec_ilv.txt).  TTS_CODEC_X3P_ILV=0 / 1 forces one (A/B)
   static const int ilv_env = getenv("TTS_CODEC_X3P_ILV") ? atoi(getenv("TTS_CODEC_X3P_ILV")) : -1;
   const bool ilv = NS == 3 || (ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64));
-  if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  // TTS_CODEC_X3P_PP=1: the out-of-phase DMA split (PP, above) on the 8-wave tile (experiment)
+  static const bool pp = getenv("TTS_CODEC_X3P_PP") && atoi(getenv("TTS_CODEC_X3P_PP"));
+  if (ilv && pp && NS == 2 && WM * WN == 8)
+    hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS, WM * WN == 8>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  else if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
   else hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
 }
 
