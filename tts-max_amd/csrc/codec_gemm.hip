@@ -222,7 +222,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   if constexpr (ILV) {
     // NS - 1 stages in flight: stage s + NS - 1 is issued while stage s is multiplied, into the
     // buffer stage s - 1 used (every wave left it: this step's barrier); one barrier per step
-    static_assert(NS == 2 || NS == 3, "two or three stage buffers");
+    static_assert(NS >= 2 && NS <= 4, "two to four stage buffers");
     constexpr int AHEAD = (NS - 2) * QD;  // pieces of the younger stages allowed in flight
 #pragma unroll
     for (int q = 0; q < NS - 1; ++q)
@@ -388,13 +388,18 @@ static void launch_x3p(const GemmF32Args& g, hipStream_t s) {
   // the small tiles, whose steps are not (one 650-code utterance 4.8 -> 5.3 ms with the first,
   // profiles/r5h_ab_codec_ilv.txt).  TTS_CODEC_X3P_ILV=0 / 1 forces one (A/B)
   static const int ilv_env = getenv("TTS_CODEC_X3P_ILV") ? atoi(getenv("TTS_CODEC_X3P_ILV")) : -1;
-  const bool ilv = NS == 3 || (ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64));
+  const bool ilv = NS >= 3 || (ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64));
   // TTS_CODEC_X3P_PP=1: the out-of-phase DMA split (PP, above) on the 8-wave tile (experiment)
   static const bool pp = getenv("TTS_CODEC_X3P_PP") && atoi(getenv("TTS_CODEC_X3P_PP"));
   if (ilv && pp && NS == 2 && WM * WN == 8)
     hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS, WM * WN == 8>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
   else if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
   else hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+}
+
+static bool small4() {
+  static const bool v = getenv("TTS_CODEC_X3P_SMALL4") && atoi(getenv("TTS_CODEC_X3P_SMALL4"));
+  return v;
 }
 
 bool gemm_x3p_supported(const GemmF32Args& g) {
@@ -419,7 +424,11 @@ void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s) {
     case 2: launch_x3p<128, 64, 2, 2>(g, s); break;
     case 3: launch_x3p<64, 64, 2, 2>(g, s); break;
     case 5: launch_x3p<128, 128, 2, 4, 3>(g, s); break;  // (8 waves of 64x32, three stages: experiment)
-    default: launch_x3p<32, 32, 1, 1>(g, s); break;  // one wave: a lone utterance's small GEMMs
+    default:  // one wave: a lone utterance's small GEMMs (TTS_CODEC_X3P_SMALL4=1: four stages, the DMA
+      // three steps ahead — experiment)
+      if (small4()) launch_x3p<32, 32, 1, 1, 4>(g, s);
+      else launch_x3p<32, 32, 1, 1>(g, s);
+      break;
   }
 }
 
