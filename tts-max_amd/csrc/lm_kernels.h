@@ -147,7 +147,7 @@ struct WgemmArgs {
   bf16_t* fo_resid = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS): [block][8]
   int csplit = 1;     // 2: each 16-column unit runs as two 8-column halves (twice the workgroups; filled in by launch_wgemm)
-  int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream
+  int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream, 64 per-wave norm-end stamps
 };
 
 struct WgemmPlan {
