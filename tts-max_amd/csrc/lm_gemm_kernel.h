@@ -655,6 +655,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
       TTS_STAMP(stp, 24);  // (wave 0: its rows normalised, before the barrier)
+      if (a.diag & kWgemmDiagMask & 64) TTS_STAMP_WAVE(stp, 8 + wave);  // (every wave, diag 64)
       __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
       __builtin_amdgcn_s_barrier();
     }
@@ -739,7 +740,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
       }
     }
 
-    if (first) { TTS_STAMP(stp, 2); TTS_STAMP_WAVE(stp, 8 + wave); }
+    if (first) {
+      TTS_STAMP(stp, 2);
+      if (!(a.diag & kWgemmDiagMask & 64)) TTS_STAMP_WAVE(stp, 8 + wave);
+    }
     if (a.diag & kWgemmDiagMask & 2) {
       if (acc[0][0][0] == 1234.5f && a.out) a.out[0] = 0;
       return;
