@@ -38,6 +38,11 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn
         m.bench_kernel(k, rows=rows, ctx=ctx, iters=1)
         assert f(buf.ctypes.data, N) == 0
     t = buf.astype(np.int64)
+    diag64 = (int(os.environ.get("TTS_WGEMM_DIAG", "0")) & 64) != 0
+    simd = None
+    if diag64:  # (the per-wave norm-end stamps carry the wave's SIMD in bits 60..61)
+        simd = (t >> 60) & 3
+        t = t & ((1 << 56) - 1)
     if k == "attention":
         st = t[16384:16384 + rows * arch.num_kv_heads * 8].reshape(-1, 8)
     else:
@@ -73,4 +78,12 @@ for k in ("qkv", "o_proj", "gate_up", "down", "attention", "qkv_attn", "qkv_attn
 
         w = us[:, 8:24]
         print(f"  waves streamed: first {q(np.nanmin(w, 1))} last {q(np.nanmax(w, 1))}  split-K barrier {q(us[:, 4])}  summed {q(us[:, 5])}")
+        if diag64 and not np.all(np.isnan(w)):  # norm end per wave: delay behind the WG's first, by wave and SIMD
+            ss = (simd[:16384].reshape(-1, 32))[t[:16384].reshape(-1, 32)[:, 0] > 0][:, 8:24]
+            d = w - np.nanmin(w, 1, keepdims=True)
+            print("  norm end behind the WG's first wave, mean us by wave: " +
+                  " ".join(f"{np.nanmean(d[:, i]):.2f}" for i in range(16)))
+            print("  ... by SIMD: " + " ".join(f"s{s}={np.nanmean(d[ss == s]):.2f}(n={int(np.sum(ss == s) / len(d))})"
+                                            for s in range(4)))
+            print("  SIMD of waves 0..15 in the first WG: " + " ".join(str(int(x)) for x in ss[0]))
     sys.stdout.flush()

@@ -410,16 +410,16 @@ bool gemm_x3p_supported(const GemmF32Args& g) {
 void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s) {
   if (!gemm_x3p_supported(g)) throw std::runtime_error("gemm_x3p: A and B planes, K % 32 == 0, 16-B aligned rows");
   // tiles: 256x128 (8 waves of 64x64, one workgroup per CU) where that makes >= 2 rounds of
-  // the CUs (the ragged batch's big GEMMs); else 128x128, 128x64 down to what fills the chip;
-  // 64x64 (4 waves) from half a round of the CUs (a lone 650-code utterance's N = 1024 GEMMs:
-  // the one-wave 32x32 tiles re-read A and B twice as often per MAC and measured slower there,
-  // profiles/r5w_ab_codec1_tile.txt); 32x32 (one wave) below that.  Every tile sweeps an
-  // output's K in the same order: the same bits.  TTS_CODEC_X3P_TILE forces one (0..5).
+  // the CUs (the ragged batch's big GEMMs); else 128x128, 128x64, 64x64 (4 waves) or 32x32 (one
+  // wave) down to what fills the chip (every tile sweeps an output's K in the same order: the
+  // same bits; a lone utterance's tile choices swept in profiles/r5w_ab_codec1_tile.txt, and
+  // 64x64 from half a round, r5z2_ab_codec1_heur.txt, measured the same).  TTS_CODEC_X3P_TILE
+  // forces one (0..5).
   static const int forced = getenv("TTS_CODEC_X3P_TILE") ? atoi(getenv("TTS_CODEC_X3P_TILE")) : -1;
   auto tiles = [&](int tm, int tn) { return ((g.M + tm - 1) / tm) * ((g.N + tn - 1) / tn); };
   int c = forced;
   if (c < 0)
-    c = tiles(256, 128) >= 512 ? 0 : tiles(128, 128) >= 256 ? 1 : tiles(128, 64) >= 256 ? 2 : tiles(64, 64) >= 128 ? 3 : 4;
+    c = tiles(256, 128) >= 512 ? 0 : tiles(128, 128) >= 256 ? 1 : tiles(128, 64) >= 256 ? 2 : tiles(64, 64) >= 256 ? 3 : 4;
   switch (c) {
     case 0: launch_x3p<256, 128, 4, 2>(g, s); break;
     case 1: launch_x3p<128, 128, 2, 2>(g, s); break;

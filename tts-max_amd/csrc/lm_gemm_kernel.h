@@ -655,7 +655,13 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         }
       }
       TTS_STAMP(stp, 24);  // (wave 0: its rows normalised, before the barrier)
-      if (a.diag & kWgemmDiagMask & 64) TTS_STAMP_WAVE(stp, 8 + wave);  // (every wave, diag 64)
+#ifdef TTS_STAMPS
+      // (diag 64: every wave's norm end, its SIMD (HW_ID bits 5:4) in the stamp's top bits)
+      if ((a.diag & 64) && stp && lane == 0) {
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        stp[8 + wave] = __builtin_amdgcn_s_memrealtime() | ((unsigned long long)((hw >> 4) & 3) << 60);
+      }
+#endif
       __builtin_amdgcn_s_waitcnt(waitcnt_lgkm0());
       __builtin_amdgcn_s_barrier();
     }
