@@ -562,9 +562,9 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const float lo = rbf(bf_lo(ne[j][q]) * rbf(bf_lo(v[q]) * r));
-              const float hi = rbf(bf_hi(ne[j][q]) * rbf(bf_hi(v[q]) * r));
-              v[q] = pack_bf2(lo, hi);
+              // (pack_bf2 rounds once: rounding the products first too would be a second,
+              // redundant round trip through v_cvt_pk_bf16_f32 + unpack — the same bits)
+              v[q] = pack_bf2(bf_lo(ne[j][q]) * rbf(bf_lo(v[q]) * r), bf_hi(ne[j][q]) * rbf(bf_hi(v[q]) * r));
             }
           }
           *(u32x4_t*)(xs + (size_t)m * ldxs + k) = v;
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             const u32x4_t g = *(const u32x4_t*)(gw + k);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+              v[q] = pack_bf2(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r), bf_hi(g[q]) * rbf(bf_hi(v[q]) * r));
             *(u32x4_t*)(xr + k) = v;
           }
         }
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
           auto scale = [&](u32x4_t& v, const u32x4_t& g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+              v[q] = pack_bf2(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r), bf_hi(g[q]) * rbf(bf_hi(v[q]) * r));
           };
           const int ks = a.K & ~(512 * SB - 1);
           for (int k0 = 0; k0 < ks; k0 += 512 * SB) {  // (SB at a time: the ring's registers are live)

@@ -29,7 +29,7 @@ __global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, int ldx, const bf16
     const u32x4_t g = *(const u32x4_t*)(w + k);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * r)));
+      v[q] = pack_bf2(bf_lo(g[q]) * rbf(bf_lo(v[q]) * r), bf_hi(g[q]) * rbf(bf_hi(v[q]) * r));
     *(u32x4_t*)(yr + k) = v;
   }
 }
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const bf16_t* __restri
       u32x4_t o;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        o[q] = pack_bf2(rbf(bf_lo(g[j][q]) * rbf(bf_lo(v[j][q]) * r)), rbf(bf_hi(g[j][q]) * rbf(bf_hi(v[j][q]) * r)));
+        o[q] = pack_bf2(bf_lo(g[j][q]) * rbf(bf_lo(v[j][q]) * r), bf_hi(g[j][q]) * rbf(bf_hi(v[j][q]) * r));
       *(u32x4_t*)(yr + c * 8) = o;
     }
   }
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void splitk_combine_norm_kernel(
     const u32x4_t g = *(const u32x4_t*)(normw + n);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      v[q] = pack_bf2(rbf(bf_lo(g[q]) * rbf(bf_lo(v[q]) * rs)), rbf(bf_hi(g[q]) * rbf(bf_hi(v[q]) * rs)));
+      v[q] = pack_bf2(bf_lo(g[q]) * rbf(bf_lo(v[q]) * rs), bf_hi(g[q]) * rbf(bf_hi(v[q]) * rs));
     *(u32x4_t*)(xn + (size_t)m * ldn + n) = v;
   }
 }
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void splitk_combine_norm_fixed_kernel(
     u32x4_t v = keep[it];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      v[q] = pack_bf2(rbf(bf_lo(g[it][q]) * rbf(bf_lo(v[q]) * rs)), rbf(bf_hi(g[it][q]) * rbf(bf_hi(v[q]) * rs)));
+      v[q] = pack_bf2(bf_lo(g[it][q]) * rbf(bf_lo(v[q]) * rs), bf_hi(g[it][q]) * rbf(bf_hi(v[q]) * rs));
     *(u32x4_t*)(xn + (size_t)m * ldn + (wave * 64 + it * 256 + lane) * 8) = v;
   }
 }
