@@ -23,7 +23,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 # wgemm_kernel<WAVES, KU, MT_MAX, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY, KSW, FROWS> launched by
 # the decode steps of the bench workloads (TTS-1 1 / 8 / 16 / 32 rows, TTS-1-Max 8 rows)
 HOT_WGEMM = [
-    "8, 2, 2, 2, 4, 1, false, 2, 2, false, 4, false",     # gate/up 17..32 rows
+    "8, 2, 2, 2, 4, 1, false, 2, 4, false, 4, false",     # gate/up 17..32 rows (four-stage ring)
     "16, 2, 1, 1, 16, 1, true, 0, 2, false, 16, true",    # QKV + attention (+ o_proj), 2..16 rows, TTS-1
     "8, 2, 2, 1, 16, 1, false, 0, 2, false, 4, false",    # K-sliced qkv / o_proj, 17..32 rows
     "16, 4, 2, 1, 16, 1, false, 0, 1, false, 16, false",  # down K chunks, 17..32 rows

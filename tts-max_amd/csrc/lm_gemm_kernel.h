@@ -1038,7 +1038,10 @@ static void launch_shape(const WgemmArgs& a, int grid, hipStream_t s) {
     // row) instead of stalling once two stages have landed: TTS-1-Max 8 rows 3,380 -> 3,370 us,
     // TTS-1 8 rows 808 -> 806 us, same ids (profiles/r4r_ab_ring4_*).  TTS_RING4=0: off
     static const bool ring4 = !(getenv("TTS_RING4") && !atoi(getenv("TTS_RING4")));
-    if (ring4 && a.M >= 4 && a.M <= 16 && S % 4 == 0) {
+    // 17..32 rows too (two m-tiles, 164 registers, no spill): gate/up 17.42 -> 17.14 us, step
+    // 993.4 -> 989.5 us at 32 rows, same ids (profiles/r5ring32_*).  TTS_RING4_32=0: 4..16 only
+    static const bool ring4_32 = !(getenv("TTS_RING4_32") && !atoi(getenv("TTS_RING4_32")));
+    if (ring4 && a.M >= 4 && a.M <= (ring4_32 ? 32 : 16) && S % 4 == 0) {
       launch_one<h.waves, h.ku, NG, h.ksplit, ASRC, NORM, EPI, 4>(a, grid, s);
       return;
     }
