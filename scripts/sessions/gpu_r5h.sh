@@ -21,4 +21,4 @@ timeout -k 10 300 python scripts/env_ab_probe.py TTS_LIB_PATH 32 1 > $O/${T}_ab_
 AB_ARCH=tts1-max timeout -k 10 400 python scripts/env_ab_probe.py TTS_LIB_PATH 8 1 > $O/${T}_ab_max8.txt 2>&1 || exit $?
 cat $O/${T}_ab_8.txt $O/${T}_ab_32.txt $O/${T}_ab_max8.txt
 unset AB_V0 AB_V1
-bash scripts/gpu_r5g.sh ${T}g
+bash scripts/sessions/gpu_r5g.sh ${T}g
