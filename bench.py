@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=30)
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the N=1 secondary lines (bs=32 batched decode, bs=8 streaming latency)")
+    ap.add_argument("--no-max-line", action="store_true",
+                    help="distributed runs: skip the TTS-1-Max 8-per-GPU line (BASELINE configs[3])")
+    ap.add_argument("--max-steps", type=int, default=2, help="timed repetitions of the TTS-1-Max sharded job")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
                     help="named BASELINE workload (sets --arch / --batch per GPU)")
     args = ap.parse_args()
@@ -327,8 +330,19 @@ def main():
         del enc
         log(f"secondary: {sec}")
 
+    # BASELINE configs[3] on the same ranks whenever the job is distributed: TTS-1-Max, 8
+    # utterances per GPU (bs=64 over 8 GPUs), the reference's contiguous rank partition
+    # (quality_validation.py:172-182) through dp.synthesize_sharded
+    if dist is not None and not args.no_max_line and args.arch == "tts1":
+        if sec is None:
+            sec = {}
+        sec["tts1max_bs64"] = tts1max_sharded(args, dist, dev, rank, world)
+        if rank == 0:
+            log(f"secondary tts1max_bs64: {sec['tts1max_bs64']}")
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # (rank 0 only, after every timed region; at N > 1 the other ranks are done)
         cpu = cpu_baseline(arch, carch, prompts_all[0], N, args)
 
     if rank == 0:
@@ -369,6 +383,77 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def tts1max_sharded(args, dist, dev, rank, world, per_gpu=8):
+    """BASELINE configs[3]: TTS-1-Max bf16, `per_gpu` utterances per GPU (64 global at 8
+    GPUs), each rank generating + voicing its contiguous shard of rank 0's broadcast request
+    batch (dp.synthesize_sharded: RCCL broadcast, ragged gathers of codes and waveforms to rank
+    0), 500 codes each.  One untimed warm-up job, then `--max-steps` jobs bracketed by barrier +
+    synchronize; codes/s = all ranks' codes / the slowest rank's time."""
+    from tts_amd import configs, dp, synth
+    from tts_amd.codec import MI355XAudioDecoder
+    from tts_amd.speechlm import MI355XSpeechLM
+
+    arch = configs.LM_ARCHS["tts1-max"]
+    carch = configs.CODEC_ARCHS[args.codec]
+    vocab = configs.vocab_for(arch)
+    N = args.new
+    G = per_gpu * world
+    prompts = [synth.synthetic_prompt(vocab, 2000 + u, args.text_tokens, args.prompt_codes) for u in range(G)]
+    P = max(len(p) for p in prompts)
+    t0 = time.time()
+    lm = MI355XSpeechLM.synthetic(arch, seed=0x5EED, device=dev.index or 0, max_batch=per_gpu,
+                                  max_seq_len=P + N + 16)
+    dec = MI355XAudioDecoder.synthetic(carch, seed=0xC0DEC, device=dev.index or 0,
+                                       max_codes=args.prompt_codes + N + 8)
+    log(f"[rank {rank}] TTS-1-Max engine ready in {time.time() - t0:.1f}s")
+    wav = torch.empty(per_gpu * (args.prompt_codes + N) * carch.samples_per_code, dtype=torch.float32, device=dev)
+    kw = dict(max_new=N, prompt_codes=lambda p: synthetic_codes(lm, p[-args.prompt_codes:]),
+              to_codes=lambda ids: synthetic_codes(lm, ids), balance="contiguous", min_new_tokens=N,
+              eos_token_id=vocab.speech_end_id, repetition_penalty=1.1, wav_out=wav)
+
+    def job():
+        _, _, (n, items) = dp.synthesize_sharded(prompts if rank == 0 else None, lm, dec, dev, **kw)
+        return n, items
+
+    job()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    n_codes, items, pre, dec_ms, steps = 0, 0, 0.0, 0.0, 0
+    for _ in range(args.max_steps):
+        n, items = job()
+        n_codes += n
+        a, b, k = lm.last_timing()
+        pre, dec_ms, steps = pre + a, dec_ms + b, steps + k
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
+    tot = torch.tensor([n_codes], dtype=torch.float64, device=dev)
+    shard = torch.tensor([items, n_codes / args.max_steps, dec_ms / max(steps, 1)], dtype=torch.float64, device=dev)
+    shards = [torch.zeros_like(shard) for _ in range(world)]
+    dist.all_gather(shards, shard)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed, total = float(el.item()), float(tot.item())
+    lm.close()
+    dec.close()
+    del lm, dec, wav
+    torch.cuda.empty_cache()
+    return dict(value=round(total / elapsed, 2), unit="audio-codes/s", n_gpus=world, global_batch=G,
+                utterances_per_gpu=per_gpu, steps=args.max_steps, ms_per_step=round(1000 * elapsed / args.max_steps, 3),
+                x_realtime=round(G * N / carch.token_rate / (elapsed / args.max_steps), 2),
+                decode_step_ms=round(dec_ms / max(steps, 1), 4), lm_prefill_ms=round(pre / args.max_steps, 3),
+                shards=[dict(rank=r, utterances=int(s[0].item()), codes=int(s[1].item()),
+                             decode_step_ms=round(float(s[2].item()), 4)) for r, s in enumerate(shards)],
+                partition="contiguous (quality_validation.py:172-182)", scaling="weak",
+                model=MODEL_NAMES["tts1-max"], codec=carch.name, codes_per_utterance=N,
+                workload=f"TTS-1-Max bf16, {per_gpu} utterances per GPU ({G} global), prompt {P} tokens, "
+                         f"{N} greedy codes each, codec {carch.name} on {args.prompt_codes + N} codes; "
+                         f"codes + waveforms gathered to rank 0 over RCCL")
 
 
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)

@@ -51,6 +51,14 @@ tts_status tts_op_sample(const float* logits, int32_t B, int32_t V, float temper
                          float top_p, uint64_t seed, int32_t step, const float* part_max, int32_t nparts,
                          float* probs, int32_t* tokens, void* stream);
 
+/* Diagnostics, no GPU needed: the kernels one decode step over `rows` rows of a model of
+ * config `cfg` would launch on a GPU of `num_cu` CUs — the engine's own step code run with
+ * its launchers in a dry-run mode (nothing allocated or launched).  Writes the unique launches
+ * in first-seen order, one per line (the weight-streaming GEMMs as
+ * "wgemm_kernel<template arguments>"), NUL-terminated, into out[cap].  The build's spill gate
+ * (tests/test_kernel_resources.py) reads its hot instantiations from here. */
+tts_status tts_debug_step_plan(const tts_lm_config* cfg, int32_t rows, int32_t num_cu, char* out, int32_t cap);
+
 /* LlamaRMSNorm over rows of x (bf16). */
 tts_status tts_op_rmsnorm(const void* x, const void* w, float eps, void* y, int32_t M, int32_t K,
                           void* stream);

@@ -106,6 +106,36 @@ def test_wgemm_norm_resid_swiglu(lib, M):
     _bf16_close(res.cpu(), ref_res, max_ulps=2, frac=0.02)
 
 
+@pytest.mark.parametrize("M", [1, 8, 24])
+def test_wgemm_norm_k_not_multiple_of_512(lib, M):
+    """K = 768 (a multiple of 256, not of 512): the LDS-DMA prologue cannot stage the rows, so
+    the op API normalises in a standalone pass first — the fused form's canonical sum order,
+    so the result equals the fused launch's arithmetic; checked against the oracle's
+    RMSNorm + nn.Linear, and row copies must agree bit for bit."""
+    K, N = 768, 1024
+    g = torch.Generator().manual_seed(768 + M)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    x[-1] = x[0]
+    nw = (1 + 0.2 * torch.randn(K, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.03).to(torch.bfloat16)
+    ref = lm_oracle.linear(lm_oracle.rmsnorm(x, nw, 1e-5), w)
+    wt = _tiled(lib, w.cuda())
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    _check(lib.tts_op_wgemm(x.cuda().data_ptr(), M, K, K, wt.data_ptr(), N, nw.cuda().data_ptr(), 1e-5,
+                            out.data_ptr(), N, None, 0, None))
+    torch.cuda.synchronize()
+    _bf16_close(out.cpu(), ref, max_ulps=3, frac=0.03)
+    assert torch.equal(out[0].cpu(), out[-1].cpu())
+
+
+def test_wgemm_rejects_matrix_beyond_buffer_range(lib):
+    """The weight stream addresses a matrix through one 32-bit buffer resource: a shape of
+    4 GiB or more is refused with an error (no launch), never silently truncated."""
+    st = lib.tts_op_wgemm(None, 1, 65536, 65536, None, 32768, None, 0.0, None, 32768, None, 0, None)
+    assert st != 0
+    assert b"unsupported" in lib.tts_last_error()
+
+
 def test_rmsnorm(lib):
     M, K = 7, 2048
     x = torch.randn(M, K).to(torch.bfloat16)

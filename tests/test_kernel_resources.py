@@ -21,25 +21,29 @@ CSRC = os.path.join(ROOT, "tts-max_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 # wgemm_kernel<WAVES, KU, MT_MAX, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY, KSW, FROWS> launched by
-# the decode steps of the bench workloads (TTS-1 1 / 8 / 16 / 32 rows, TTS-1-Max 8 rows)
-HOT_WGEMM = [
-    "8, 2, 2, 2, 4, 1, false, 2, 4, false, 4, false",     # gate/up 17..32 rows (four-stage ring)
-    "16, 2, 1, 1, 16, 1, true, 0, 2, false, 16, true",    # QKV + attention (+ o_proj), 2..16 rows, TTS-1
-    "8, 2, 2, 1, 16, 1, false, 0, 2, false, 4, false",    # K-sliced qkv / o_proj, 17..32 rows
-    "16, 4, 2, 1, 16, 1, false, 0, 1, false, 16, false",  # down K chunks, 17..32 rows
-    "8, 2, 1, 2, 4, 1, true, 2, 4, false, 4, false",      # gate/up 4..16 rows (four-stage ring)
-    "4, 8, 2, 1, 1, 1, false, 3, 2, false, 1, false",     # lm_head 17..32 rows
-    "16, 4, 1, 1, 16, 1, false, 1, 2, false, 16, false",  # down 2..16 rows
-    "8, 2, 1, 2, 4, 1, true, 2, 2, true, 4, false",       # gate/up one row
-    "16, 2, 1, 1, 16, 1, true, 0, 2, true, 16, false",    # QKV + attention + o_proj one row
-    "4, 8, 1, 1, 1, 1, true, 3, 2, false, 1, false",      # lm_head 2..16 rows
-    "16, 4, 1, 1, 16, 1, false, 1, 2, true, 16, false",   # down one row
-    "4, 8, 1, 1, 1, 1, true, 3, 2, true, 1, false",       # lm_head one row
-    "16, 2, 1, 1, 16, 1, false, 1, 2, true, 16, false",   # o_proj one row (separate launch)
-    "16, 4, 1, 1, 16, 1, true, 0, 2, false, 16, true",    # TTS-1-Max QKV + attention + o_proj, 8 rows
-    "16, 4, 1, 1, 16, 0, false, 1, 1, false, 16, false",  # TTS-1-Max down (A fragments from L2), 8 rows
-    "16, 4, 1, 1, 16, 1, true, 0, 2, false, 16, false",   # TTS-1-Max QKV (separate launch), 8 rows
-]
+# the decode steps of the bench workloads and their neighbours, read from the engine's own step
+# code in dry-run mode (tts_debug_step_plan): a new plan shape cannot escape the gate.
+# (arch, decode rows): TTS-1 at configs[1]'s one row, configs[4]'s 8, configs[2]'s 32 and the
+# row counts between / beyond them; TTS-1-Max at configs[3]'s 8 per GPU, 1 and 16
+PLAN_CASES = [("tts1", r) for r in (1, 2, 4, 8, 12, 16, 17, 24, 32, 48, 64)] + \
+             [("tts1-max", r) for r in (1, 8, 16, 32)]
+
+
+def _hot_wgemm():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tts-max_amd"))
+    from tts_amd import configs
+    from tts_amd.speechlm import step_plan
+
+    hot = {}
+    for arch, rows in PLAN_CASES:
+        for k in step_plan(configs.LM_ARCHS[arch], rows):
+            if k.startswith("wgemm_kernel<"):
+                hot.setdefault(k[len("wgemm_kernel<"):-1], f"{arch} {rows} rows")
+    return hot
+
+
 UNITS = ["lm_gemm_store.hip", "lm_gemm_resid.hip", "lm_gemm_swiglu.hip", "lm_gemm_logits.hip", "lm_attn.hip",
          "lm_ops.hip", "codec_kernels.hip", "codec_gemm.hip"]
 
@@ -82,11 +86,30 @@ def spills():
     return names
 
 
+def test_step_plan_lists_the_bench_launches():
+    """The dry run reproduces the launch structure the GPU runs: the one-row step is three
+    launches a layer + lm_head + finalize (QKV + attention + o_proj fused, gate/up, down)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tts-max_amd"))
+    from tts_amd import configs
+    from tts_amd.speechlm import step_plan
+
+    one = step_plan(configs.LM_ARCHS["tts1"], 1)
+    assert one[-1] == "finalize_greedy_kernel"
+    assert len([k for k in one if k.startswith("wgemm_kernel<")]) == 4, one
+    assert "attn_decode_kernel<64>" not in one  # (fused into the QKV launch)
+    b32 = step_plan(configs.LM_ARCHS["tts1"], 32)
+    assert "attn_decode_kernel<64>" in b32 and "splitk_combine_norm" in b32, b32
+
+
 def test_hot_wgemm_instantiations_do_not_spill(spills):
-    found = {h: spills[_mangled(h)][1] for h in HOT_WGEMM if _mangled(h) in spills}
-    missing = [h for h in HOT_WGEMM if h not in found]
+    hot = _hot_wgemm()
+    assert len(hot) >= 10, hot
+    found = {h: spills[_mangled(h)][1] for h in hot if _mangled(h) in spills}
+    missing = {h: hot[h] for h in hot if h not in found}
     assert not missing, f"hot instantiations not compiled: {missing}"
-    bad = {h: n for h, n in found.items() if n > 0}
+    bad = {h: (n, hot[h]) for h, n in found.items() if n > 0}
     assert not bad, f"VGPR spills in hot-path GEMM instantiations: {bad}"
 
 

@@ -2,6 +2,7 @@
 // Every entry point catches everything: errors become a status code plus a thread-local
 // message, never an exception across the ABI.
 #include <stdlib.h>
+#include <string.h>
 
 #include <memory>
 #include <string>
@@ -240,6 +241,15 @@ tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32
   });
 }
 
+tts_status tts_debug_step_plan(const tts_lm_config* cfg, int32_t rows, int32_t num_cu, char* out, int32_t cap) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && out && cap > 0, "null argument");
+    const std::string p = lm_step_plan(*cfg, rows, num_cu);
+    TTS_REQUIRE((int64_t)p.size() < cap, "output buffer too small");
+    memcpy(out, p.c_str(), p.size() + 1);
+  });
+}
+
 tts_status tts_codec_load(tts_engine* e, const tts_codec_config* cfg, const tts_tensor_desc* t,
                           int32_t n) {
   return guarded([&] {
@@ -345,21 +355,31 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
     TTS_REQUIRE(wgemm_supported(M, N, K, epi), "unsupported GEMM shape");
     TTS_REQUIRE(ldx == K, "ldx must equal K");
     WgemmPlan p = plan_wgemm(M, N, K, epi, device_cu_count());
-    TTS_REQUIRE(normw == nullptr || (p.a_lds && !p.sliced && K <= 4096),
-                "fused RMSNorm needs M*K small enough for LDS and K <= 4096");
+    hipStream_t st = (hipStream_t)stream;
     WgemmArgs a;
     a.x = (const bf16_t*)x; a.M = M; a.K = K; a.ldx = ldx;
     a.w = (const bf16_t*)w_tiled; a.N = N;
     a.normw = (const bf16_t*)normw; a.eps = eps;
     a.out = (bf16_t*)out; a.ldo = ldo; a.resid = (bf16_t*)resid;
+    // RMSNorm in the GEMM's prologue where the rows fit it (LDS rows, K <= 4096, the LDS-DMA
+    // pieces of 512 columns); otherwise a standalone pass first — the same canonical sum order
+    // (chunk_sumsq), so the same bits either way, as the engine does (lm_engine.cpp gemm)
+    bf16_t* xn = nullptr;
+    if (normw && !(p.a_lds && !p.sliced && K <= 4096 && K % 512 == 0)) {
+      HIP_CHECK(hipMallocAsync((void**)&xn, (size_t)M * K * 2, st));
+      launch_rmsnorm(a.x, ldx, a.normw, eps, xn, K, M, K, st);
+      a.x = xn;
+      a.normw = nullptr;
+    }
     float* part = nullptr;
     if (p.sliced) {
-      HIP_CHECK(hipMallocAsync((void**)&part, wgemm_part_elems(p, M, ldo) * 4, (hipStream_t)stream));
+      HIP_CHECK(hipMallocAsync((void**)&part, wgemm_part_elems(p, M, ldo) * 4, st));
       a.part_out = part;
     }
-    launch_wgemm(a, p, epi, normw != nullptr && !p.sliced, (hipStream_t)stream);
+    launch_wgemm(a, p, epi, a.normw != nullptr, st);
     HIP_CHECK(hipGetLastError());
-    if (part) HIP_CHECK(hipFreeAsync(part, (hipStream_t)stream));
+    if (part) HIP_CHECK(hipFreeAsync(part, st));
+    if (xn) HIP_CHECK(hipFreeAsync(xn, st));
   });
 }
 

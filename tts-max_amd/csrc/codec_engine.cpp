@@ -336,9 +336,12 @@ void gemm_p(const uint16_t* Ap, long long ap_plane, int M, int K, int lda, const
   launch_gemm_x3p(g, s);
 }
 
-// TTS_CODEC_X3P=0: the fp32-staging GEMM (gemm_bx3_kernel splits A while staging) everywhere
+// TTS_CODEC_X3P=0: the fp32-staging GEMM (gemm_bx3_kernel splits A while staging) everywhere.
+// TTS_CODEC_BX3=0 (plain fp32 MFMA for every contraction, a debugging switch) turns the
+// split-bf16 x3p path off as well
 bool use_x3p() {
-  static const bool v = !(getenv("TTS_CODEC_X3P") && !atoi(getenv("TTS_CODEC_X3P")));
+  static const bool v = !(getenv("TTS_CODEC_X3P") && !atoi(getenv("TTS_CODEC_X3P"))) &&
+                        !(getenv("TTS_CODEC_BX3") && !atoi(getenv("TTS_CODEC_BX3")));
   return v;
 }
 

@@ -86,9 +86,6 @@ struct LmWork {
   DevBuf blocks;                                    // prefill query blocks (int4, lm_attn.hip)
   int nblocks = 0;
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
-  DevBuf apart;                                     // split decode attention partials (AttnArgs::part)
-  int attn_splits = 0;                              // chunks per (row, kv head) of the batched decode attention
-  bool attn_splits_on() const { return attn_splits > 1; }
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
@@ -166,6 +163,7 @@ void lm_score_decode(Engine* e, const int32_t* ids, const int32_t* lens, int B, 
                      const int32_t* gidx, int k, float* out, hipStream_t s);
 void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* avg_ms,
                      double* bytes);
+std::string lm_step_plan(const tts_lm_config& c, int rows, int num_cu);
 
 // upload a named tensor to device memory as bf16 (convert from f32 if needed)
 void upload_bf16(const tts_tensor_desc& d, bf16_t* dst, hipStream_t s, DevBuf& staging);

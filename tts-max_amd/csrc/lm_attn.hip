@@ -126,95 +126,8 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
   }
 }
 
-// ------------------------------------------------------------- split decode (batched) -----
-// Workgroup = one chunk of one (row, kv head): SPLIT_NW waves of 32 positions per pass
-// (lm_attn_core.h dec_chunk).  The chunk length is ceil(ctx / splits) rounded up to 32, so
-// every step's workgroups share the context evenly whatever its length (the grid is fixed
-// in the captured step).  The workgroup whose chunk holds the new position appends its k / v.
-constexpr int SPLIT_NW = 4, SPLIT_PW = 32;
-template <int D> constexpr int split_part_floats() { return 2 * DEC_G + DEC_G * D; }
-
-template <int D>
-__global__ __launch_bounds__(SPLIT_NW * 64) void attn_split_kernel(AttnArgs a) {
-  constexpr int PW = SPLIT_PW, NW = SPLIT_NW;
-  using C = DecShape<D, PW>;
-  __shared__ __attribute__((aligned(16))) float qs[DEC_G * D];
-  __shared__ __attribute__((aligned(16))) bf16_t knew[D];
-  __shared__ __attribute__((aligned(16))) bf16_t vnew[D];
-  __shared__ __attribute__((aligned(16))) float red[dec_red_floats<D, NW>()];
-  const int ns = a.splits;
-  const int pair = blockIdx.x / ns, ch = blockIdx.x - pair * ns;
-  const int row = pair / a.KVH, kvh = pair - row * a.KVH;
-  const int slot = a.row_slot[row], pos = a.row_pos[row], ctx = pos + 1;
-  const int clen = ((ctx + ns - 1) / ns + PW - 1) / PW * PW;
-  const int p0 = ch * clen, lim = min(ctx, p0 + clen);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const size_t kvbase = ((size_t)slot * a.KVH + kvh) * a.max_seq * D;
-  const bf16_t* kc = a.kcache + kvbase;
-  const bf16_t* vtc = a.vtcache + kvbase;
-  float* part = a.part + (size_t)blockIdx.x * split_part_floats<D>();
-  u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
-  if (p0 + wave * PW < lim) {  // this wave's first-pass fragments before anything else
-    dec_load_k<D, PW>(kc, p0 + wave * PW, lim, lane, kf);
-    dec_load_v<D, PW>(vtc, a.max_seq, p0 + wave * PW, lane, vf);
-  }
-  const bf16_t* qrow = a.qkv + (size_t)row * a.ld_qkv;
-  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
-  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
-  for (int i = tid; i < DEC_G * D + D; i += NW * 64) {
-    if (i < DEC_G * D) {
-      const int g = i / D, d = i % D;
-      qs[i] = rope_at<D>(qrow + (kvh * DEC_G + g) * D, d, cosr, sinr);
-    } else {
-      const int d = i - DEC_G * D;
-      knew[d] = f2bf(rope_at<D>(qrow + a.H * D + kvh * D, d, cosr, sinr));
-      vnew[d] = qrow[a.H * D + a.KVH * D + kvh * D + d];
-    }
-  }
-  lds_barrier();
-  if (p0 >= ctx) {  // (short contexts: trailing chunks are empty)
-    for (int i = tid; i < split_part_floats<D>(); i += NW * 64) part[i] = i < DEC_G ? -INFINITY : 0.f;
-    return;
-  }
-  dec_chunk<D, PW, NW>(kc, vtc, a.max_seq, p0, lim, ctx, a.scale, qs, knew, vnew, red, kf, vf, part);
-  if (lim == ctx && tid < D) {  // the chunk holding the new position appends it, after its reads
-    a.kcache[kvbase + (size_t)pos * D + tid] = knew[tid];
-    a.vtcache[kvbase + (size_t)tid * a.max_seq + pos] = vnew[tid];
-  }
-}
-
-// out[row][(kvh*4 + h)*D + d] = sum_c O_c e^(m_c - M) / sum_c l_c e^(m_c - M), chunks in order
-template <int D>
-__global__ __launch_bounds__(DEC_G * D) void attn_merge_kernel(AttnArgs a) {
-  const int ns = a.splits, pair = blockIdx.x;
-  const int row = pair / a.KVH, kvh = pair - row * a.KVH;
-  const int t = threadIdx.x, h = t / D;
-  const float* pp = a.part + (size_t)pair * ns * split_part_floats<D>();
-  float M = -INFINITY;
-  for (int c = 0; c < ns; ++c) M = fmaxf(M, pp[(size_t)c * split_part_floats<D>() + h]);
-  float L = 0.f, O = 0.f;
-  for (int c = 0; c < ns; ++c) {
-    const float* q = pp + (size_t)c * split_part_floats<D>();
-    const float e = __builtin_amdgcn_exp2f((q[h] - M) * 1.44269504088896341f);  // (empty chunk: 2^-inf = 0)
-    L += q[DEC_G + h] * e;
-    O += q[2 * DEC_G + t] * e;
-  }
-  a.out[(size_t)row * a.H * D + kvh * DEC_G * D + t] = f2bf(O / L);
-}
-
 void launch_attn_decode_step(const AttnArgs& a, hipStream_t s) {
-  if (a.splits > 1) {
-    const dim3 g1(a.rows * a.KVH * a.splits), g2(a.rows * a.KVH);
-    if (a.D == 64) {
-      hipLaunchKernelGGL((attn_split_kernel<64>), g1, dim3(SPLIT_NW * 64), 0, s, a);
-      hipLaunchKernelGGL((attn_merge_kernel<64>), g2, dim3(DEC_G * 64), 0, s, a);
-    } else {
-      hipLaunchKernelGGL((attn_split_kernel<128>), g1, dim3(SPLIT_NW * 64), 0, s, a);
-      hipLaunchKernelGGL((attn_merge_kernel<128>), g2, dim3(DEC_G * 128), 0, s, a);
-    }
-    return;
-  }
+  if (dry_record(a.D == 64 ? "attn_decode_kernel<64>" : "attn_decode_kernel<128>")) return;
   const dim3 grid(a.rows * a.KVH);
   if (a.D == 64) hipLaunchKernelGGL((attn_decode_kernel<64>), grid, dim3(dec_nw<64>() * 64), 0, s, a);
   else hipLaunchKernelGGL((attn_decode_kernel<128>), grid, dim3(dec_nw<128>() * 64), 0, s, a);

@@ -325,106 +325,6 @@ TTS_DEV void dec_attend(const bf16_t* kc, const bf16_t* vtc, int S, int ctx, flo
                           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x, bar, stp, gout, gtag);
 }
 
-// ---------------------------------------------------- split decode attention (batched) -----
-// One chunk [p0, lim) of the context of one (row, kv head) by the NW waves of a workgroup, as
-// a flash-decoding partial: the chunk's own maximum m per head, p = exp(s - m) (rounded to
-// bf16 for P.V, as in dec_attend), l = sum p, O = P.V unnormalised (fp32).  ctx = the row's
-// whole context (the new position ctx - 1 is patched in from knew / vnew wherever a fragment
-// spans it).  Writes part = {m[4], l[4], O[4][D]}; an empty chunk writes m = -inf, l = O = 0.
-// The merge (attn_merge_kernel) rescales by exp(m - M) with M the maximum over the chunks, so
-// the result differs from dec_attend's single-maximum form only by where p is rounded (the
-// FlashAttention-2 form).
-template <int D, int PW, int NW>
-TTS_DEV void dec_chunk(const bf16_t* kc, const bf16_t* vtc, int S, int p0, int lim, int ctx, float scale,
-                       const float* qs, const bf16_t* knew, const bf16_t* vnew, float* red,
-                       u32x4_t (&kf0)[DecShape<D, PW>::MT][DecShape<D, PW>::KS],
-                       u32x4_t (&vf0)[DecShape<D, PW>::PS][DecShape<D, PW>::DT], float* part) {
-  using C = DecShape<D, PW>;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c = lane & 15, g = lane >> 4;
-  const int npass = (lim - p0 + NW * PW - 1) / (NW * PW);
-  float* mred = red;
-  float* lred = red + NW * DEC_G;
-  float* ored = lred + NW * DEC_G;
-  const int base0 = p0 + wave * PW;
-  f32x4_t s0[C::MT];
-  float mx = -INFINITY;
-  if (base0 < lim) {
-    dec_patch_k<D, PW>(base0, ctx, lane, knew, kf0);
-    dec_patch_v<D, PW>(base0, ctx, lane, vnew, vf0);
-    dec_scores<D, PW>(kf0, qs, base0, lim, scale, lane, s0);
-#pragma unroll
-    for (int mt = 0; mt < C::MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s0[mt][r]);
-  }
-  for (int ps = 1; ps < npass; ++ps) {
-    const int base = p0 + (ps * NW + wave) * PW;
-    if (base >= lim) break;
-    u32x4_t kf[C::MT][C::KS];
-    dec_load_k<D, PW>(kc, base, lim, lane, kf);
-    dec_patch_k<D, PW>(base, ctx, lane, knew, kf);
-    f32x4_t sc[C::MT];
-    dec_scores<D, PW>(kf, qs, base, lim, scale, lane, sc);
-#pragma unroll
-    for (int mt = 0; mt < C::MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[mt][r]);
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  if (lane < DEC_G) mred[wave * DEC_G + lane] = mx;
-  lds_barrier();
-  float M = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) M = fmaxf(M, mred[w * DEC_G + (c & 3)]);
-  float lsum = 0.f;
-  f32x4_t o[C::DT];
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt) o[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  if (base0 < lim) dec_pv<D, PW>(M, lsum, s0, vf0, o);
-  for (int ps = 1; ps < npass; ++ps) {
-    const int base = p0 + (ps * NW + wave) * PW;
-    if (base >= lim) break;
-    u32x4_t kf[C::MT][C::KS], vf[C::PS][C::DT];
-    dec_load_v<D, PW>(vtc, S, base, lane, vf);
-    dec_load_k<D, PW>(kc, base, lim, lane, kf);
-    dec_patch_k<D, PW>(base, ctx, lane, knew, kf);
-    f32x4_t sc[C::MT];
-    dec_scores<D, PW>(kf, qs, base, lim, scale, lane, sc);
-    dec_patch_v<D, PW>(base, ctx, lane, vnew, vf);
-    dec_pv<D, PW>(M, lsum, sc, vf, o);
-  }
-  lsum += __shfl_xor(lsum, 16, 64);
-  lsum += __shfl_xor(lsum, 32, 64);
-  if (c < DEC_G) {
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-      *(float4*)(ored + (wave * DEC_G + c) * D + 16 * dt + 4 * g) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
-    if (g == 0) lred[wave * DEC_G + c] = lsum;
-  }
-  lds_barrier();
-  // (waves past the chunk hold l = 0, O = 0: their sums add nothing)
-  for (int i = tid; i < DEC_G * D; i += NW * 64) {
-    const int h = i / D, d = i - h * D;
-    float v[NW];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) v[w] = ored[(w * DEC_G + h) * D + d];
-    float O = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) O += v[w];
-    part[2 * DEC_G + i] = O;
-  }
-  if (tid < DEC_G) {
-    float L = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) L += lred[w * DEC_G + tid];
-    part[tid] = M;  // (-inf for an empty chunk: every score masked)
-    part[DEC_G + tid] = L;
-  }
-}
-
 // RoPE of one element (HF apply_rotary_pos_emb in bf16: x*cos + rotate_half(x)*sin, each
 // op rounded to bf16): x = element d, xr = element d +- D/2 (its rotate_half partner)
 TTS_DEV float rope_elem(bf16_t x, bf16_t xr, bool lower_half, float c, float sn) {

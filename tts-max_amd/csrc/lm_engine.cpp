@@ -121,6 +121,13 @@ void compute_rope_table(const tts_lm_config& c, std::vector<bf16_t>& cs, std::ve
 }
 }  // namespace
 
+// K-sliced GEMMs (store / residual epilogues): fp32 partials of kc = K / 2048 chunks of <= 64 rows
+static size_t kpart_bytes(const tts_lm_config& c) {
+  const int kmax = std::max(c.hidden_size, std::max(c.intermediate_size, c.num_heads * c.head_dim));
+  const int QKV = (c.num_heads + 2 * c.num_kv_heads) * c.head_dim;
+  return (size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, c.hidden_size) * 4;
+}
+
 void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int n) {
   TTS_REQUIRE(cfgp != nullptr, "null config");
   const tts_lm_config c = *cfgp;
@@ -245,21 +252,8 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.gran.alloc((size_t)std::max(B, 2) * (QKV + H * D) / 2 * 8);  // q|k|v, then attention rows
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
-  {  // batched decode attention split over the context (flash-decoding chunks + merge kernel,
-     // lm_attn.hip): measured slower than one workgroup per (row, kv head) at TTS-1's 8 and 32
-     // rows (8.8 -> 10.4-11.2 us, 9.4 -> 17.1-17.8 us; profiles/r4c_ab_split*.txt) and at
-     // TTS-1-Max's 8 rows (12.0 -> 9.0 + 5.0 us merge, profiles/r4c_tts1max_bs8_kernel_stats.csv),
-     // so off by default; TTS_ATTN_SPLIT=<n>: n chunks per (row, kv head)
-    const char* ev = getenv("TTS_ATTN_SPLIT");
-    int ns = ev ? std::min(16, atoi(ev)) : 1;
-    w.attn_splits = ns;
-    if (ns > 1) w.apart.alloc((size_t)B * KVH * ns * (8 + 4 * D) * 4);
-  }
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
-  {  // K-sliced GEMMs (store / residual epilogues): kc = K / 2048 chunks of <= 64 rows
-    const int kmax = std::max(HID, std::max(FF, H * D));
-    w.kpart.alloc((size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, HID) * 4);
-  }
+  w.kpart.alloc(kpart_bytes(c));
   w.slogits.alloc((size_t)B * V * 4);
   w.counts.alloc((size_t)B * (V / 32 + 1) * 32 * 2);
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
@@ -313,8 +307,8 @@ bool use_fused_oproj() {
   return v;
 }
 
-// 17..32 rows: RMSNorm in the GEMM's LDS prologue (rows landed by LDS-DMA, a wave per row)
-// instead of a standalone launch — experiment hook TTS_NORM32=1 (round 2 measured it slower)
+// 17..32 rows: the decode attention sums the K-sliced QKV partials (no combine launch);
+// TTS_QKV_DEFER=0 keeps the combine launch (same sums in the same order: the same bits)
 bool use_qkv_defer() {
   static const bool v = !(getenv("TTS_QKV_DEFER") && !atoi(getenv("TTS_QKV_DEFER")));
   return v;
@@ -323,20 +317,10 @@ bool use_kslice32() {
   static const bool v = !(getenv("TTS_KSLICE32") && !atoi(getenv("TTS_KSLICE32")));
   return v;
 }
-// ... for the residual projection (o_proj) alone: TTS_KSLICE32_RESID=0 runs it unsliced (the A
-// rows staged whole, the residual epilogue writes the hidden rows: no combine launch)
-bool use_kslice32_resid() {
-  static const bool v = !(getenv("TTS_KSLICE32_RESID") && !atoi(getenv("TTS_KSLICE32_RESID")));
-  return v;
-}
 // ... and at 2..16 rows, o_proj fused behind the attention of the QKV launch (its own
 // workgroups after the attention's): default on; TTS_FUSED_OPROJ_ROWS=0 keeps the launch
 bool use_fused_oproj_rows() {
   static const bool v = !(getenv("TTS_FUSED_OPROJ_ROWS") && !atoi(getenv("TTS_FUSED_OPROJ_ROWS")));
-  return v;
-}
-bool norm_in_lds32() {
-  static const bool v = getenv("TTS_NORM32") && atoi(getenv("TTS_NORM32"));
   return v;
 }
 
@@ -398,7 +382,7 @@ struct Ctx {
       if (norm && rows > 16 && normw == ready && x == w.x.as<bf16_t>()) {
         xin = w.xn.as<bf16_t>() + (size_t)r0 * K;
         norm = false;
-      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || (rows > 16 && !norm_in_lds32()))) {
+      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || rows > 16)) {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
@@ -409,7 +393,7 @@ struct Ctx {
       // (chosen by the batch's row count, not the chunk's: a 33..64-row batch runs two chunks,
       // and every row of a batch must take the same arithmetic)
       if (!norm && rows > 16 && m <= 32 && K == 2048 && !logit_extra &&
-          (epi == EPI_STORE || (epi == EPI_RESID && use_kslice32_resid())) && use_kslice32() && p.sp.kc == 1 && p.sp.waves == 16 && p.sp.ksplit == 16 && p.sp.ku == 2 && p.sp.ng == 1 &&
+          (epi == EPI_STORE || epi == EPI_RESID) && use_kslice32() && p.sp.kc == 1 && p.sp.waves == 16 && p.sp.ksplit == 16 && p.sp.ku == 2 && p.sp.ng == 1 &&
           (size_t)4 * m * ldo * 4 <= w.kpart.bytes) {
         WgemmArgs a;
         a.x = xin; a.M = m; a.K = K / 4; a.ldx = K;
@@ -476,10 +460,6 @@ struct Ctx {
     a.q_rot = w.q_rot.as<bf16_t>(); a.out = w.attn_out.as<bf16_t>();
     a.blocks = w.blocks.as<int4>(); a.nblocks = w.nblocks;
     a.stamps = stamp_buf();
-    if (decode && rows > 1 && w.attn_splits > 1) {  // (one row: the fused launch's single-workgroup form)
-      a.splits = w.attn_splits;
-      a.part = w.apart.as<float>();
-    }
     if (decode && qkv_part_pending) {
       a.qkv_part = w.kpart.as<float>();
       a.qkv_nsl = 4;
@@ -566,7 +546,7 @@ struct Ctx {
              EPI_STORE, &fx);
       } else {
         // (defer: TTS_QKV_DEFER=0 keeps the combine launch)
-        defer_qkv_combine = decode && rows > 16 && rows <= 32 && use_qkv_defer() && !w.attn_splits_on();
+        defer_qkv_combine = decode && rows > 16 && rows <= 32 && use_qkv_defer();
         qkv_part_pending = false;
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE);
@@ -1280,6 +1260,56 @@ void lm_score_decode(Engine* e, const int32_t* ids, const int32_t* lens, int B, 
     }
   }
   check_fattn(e, s);
+}
+
+// The launch list of one decode step over `rows` rows of a model of config c on num_cu CUs,
+// without a GPU: the step's own code (Ctx::layers + head_and_pick) run with the launchers in
+// dry-run mode (lm_kernels.h dry_launches), nothing allocated.  Unique launches in first-seen
+// order, one per line (wgemm instantiations as wgemm_inst_name writes them).
+std::string lm_step_plan(const tts_lm_config& c, int rows, int num_cu) {
+  TTS_REQUIRE(c.head_dim == 64 || c.head_dim == 128, "head_dim must be 64 or 128");
+  TTS_REQUIRE(c.num_heads == 4 * c.num_kv_heads && c.num_layers >= 1, "bad config");
+  TTS_REQUIRE(rows >= 1 && rows <= 64 && num_cu >= 1, "rows in [1, 64], num_cu >= 1");
+  Engine e;  // (no HIP call: no stream, no buffer)
+  e.num_cu = num_cu;
+  e.lm.cfg = c;
+  e.lm.cfg.max_batch = std::max(c.max_batch, rows);
+  // distinct placeholder addresses for the weights (the step code compares norm-weight pointers
+  // to choose its RMSNorm form; nothing is dereferenced in a dry run)
+  uintptr_t fake = 0x10000;
+  auto next = [&] { fake += 0x100; return (bf16_t*)fake; };
+  e.lm.layers.resize(c.num_layers);
+  for (LmLayer& ly : e.lm.layers) {
+    ly.ln1 = next(); ly.ln2 = next(); ly.wqkv = next(); ly.wo = next(); ly.wgu = next(); ly.wd = next();
+  }
+  e.lm.final_norm = next();
+  e.lm.lm_head = next();
+  e.w.cap_batch = e.lm.cfg.max_batch;
+  e.w.kpart.bytes = kpart_bytes(c);  // (the size the plan checks; never dereferenced)
+  std::vector<std::string> rec;
+  dry_launches() = &rec;
+  try {
+    Ctx X(&e, nullptr);
+    X.layers(rows, nullptr, nullptr, true);
+    const StepState st = X.state(rows, 0, 0);
+    tts_gen_params gp{};
+    gp.repetition_penalty = 1.1f;
+    X.head_and_pick(nullptr, rows, st, gp);
+  } catch (...) {
+    dry_launches() = nullptr;
+    e.w.kpart.bytes = 0;
+    throw;
+  }
+  dry_launches() = nullptr;
+  e.w.kpart.bytes = 0;
+  std::string out;
+  std::vector<std::string> seen;
+  for (const std::string& r : rec)
+    if (std::find(seen.begin(), seen.end(), r) == seen.end()) {
+      seen.push_back(r);
+      out += r + "\n";
+    }
+  return out;
 }
 
 }  // namespace tts

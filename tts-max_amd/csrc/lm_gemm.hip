@@ -27,6 +27,11 @@
 
 namespace tts {
 
+std::vector<std::string>*& dry_launches() {
+  static thread_local std::vector<std::string>* rec = nullptr;
+  return rec;
+}
+
 // ---------------------------------------------------------------- weight re-layout ----
 __global__ void retile_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ t, int N,
                               int K, int nt_mult, int nt_off, StreamPlan p, int units) {
@@ -152,17 +157,9 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   static const bool agr_on = !(getenv("TTS_AGR") && !atoi(getenv("TTS_AGR")));
   if (agr_on && M <= 16 && epi == EPI_RESID && !p.a_lds && p.sp.kc > 1 && p.grid * p.sp.kc > 2 * num_cu)
     return p;  // a_lds = false, unsliced
-  // 17..32 rows, K in one chunk, plain store / residual (TTS-1 qkv, o_proj): each wave loading
-  // its own A fragments beside its weight tiles (A_GLOBAL ring, L2 hits) instead of every
-  // workgroup staging all 32 A rows (128 KiB) into LDS — measured slower (qkv 10.6 -> 15.5 us,
-  // o_proj 8.7 -> 12.0 us, bs=32 step 1.21 -> 1.36 ms; profiles/r4c_ab_agr32.txt: the
-  // fragment-shaped L2 loads cost more than the full-line LDS-DMA).  Experiment hook TTS_AGR32=1
-  static const bool agr32 = getenv("TTS_AGR32") && atoi(getenv("TTS_AGR32"));
-  bool agr_rows32 = false;
-  if (agr32 && M > 16 && M <= 32 && p.sp.kc == 1 && (epi == EPI_STORE || epi == EPI_RESID) && p.sp.ku <= 2) {
-    p.a_lds = false;
-    agr_rows32 = true;
-  }
+  // (17..32 rows with A fragments from L2 beside the weight tiles instead of the LDS rows,
+  // the RMSNorm in the LDS prologue, and column halves at 17..32 rows were measured slower and
+  // removed in round 6: profiles/r4c_ab_agr32.txt, r2_ab_norm32.txt)
   if (!p.a_lds && p.sp.kc > 1 && (epi == EPI_STORE || epi == EPI_RESID) &&
       wgemm_lds_bytes(w, ks, ng, M, K / p.sp.kc, true) <= kLdsBudget) {
     p.a_lds = true;
@@ -181,11 +178,7 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   static const int csplit_mode = getenv("TTS_CSPLIT") ? atoi(getenv("TTS_CSPLIT")) : 1;
   const int units = (N / 16) / ng;
   const int upw = w / ks;
-  // (17..32 rows with A from L2: the halves' waves load the same A fragments, L2 hits;
-  // TTS_CSPLIT32=0: off)
-  static const bool csplit32 = !(getenv("TTS_CSPLIT32") && !atoi(getenv("TTS_CSPLIT32")));
-  if (csplit_mode > 0 && (M <= 16 || csplit_mode == 2 || (agr_rows32 && csplit32)) && !p.sliced &&
-      (p.a_lds || agr_rows32) &&
+  if (csplit_mode > 0 && (M <= 16 || csplit_mode == 2) && !p.sliced && p.a_lds &&
       (epi == EPI_STORE || epi == EPI_RESID) && p.grid * upw >= units && 2 * units <= num_cu * upw) {
     p.csplit = 2;
     p.grid = (2 * units + upw - 1) / upw;
@@ -217,7 +210,11 @@ bool wgemm_fattn_rows_ok(int M, int N, int K, int D, int num_cu) {
 
 bool wgemm_supported(int M, int N, int K, int epi) {
   const int NG = (epi == EPI_SWIGLU) ? 2 : 1;
-  return M >= 1 && M <= 64 && (N % (16 * NG)) == 0 && (K % 256) == 0;
+  // (the weight stream addresses the tiled matrix through one buffer resource: 32-bit byte
+  // offsets, and the out-of-range sentinel of the refills past a wave's last unit must stay
+  // beyond the matrix, wgemm_kernel)
+  return M >= 1 && M <= 64 && N > 0 && K > 0 && (N % (16 * NG)) == 0 && (K % 256) == 0 &&
+         (unsigned long long)N * (unsigned long long)K * 2ull <= kWgemmMaxBytes;
 }
 
 void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p_in, int epi, bool norm, hipStream_t s) {
@@ -238,12 +235,14 @@ void launch_wgemm(const WgemmArgs& a_in, const WgemmPlan& p_in, int epi, bool no
   if (p.sliced) {
     // one K chunk per workgroup row of the grid: fp32 partials, then the epilogue in a
     // combine kernel (fixed chunk order: deterministic)
-    if (norm || (epi != EPI_STORE && epi != EPI_RESID) || a.part_out == nullptr)
+    if (norm || (epi != EPI_STORE && epi != EPI_RESID) || (a.part_out == nullptr && !dry_launches()))
       throw std::runtime_error("K-sliced wgemm: store/residual epilogues with a partial workspace only");
     const int Kfull = a.K;
     a.K = Kfull / p.sp.kc;  // the kernel's A chunk; ldx stays the full row
     launch_wgemm_store(a, p, false, s);
-    if (epi == EPI_RESID && a.next_norm && a.norm_out)
+    if (epi == EPI_RESID && a.next_norm && !a.norm_out && !dry_launches())
+      throw std::runtime_error("K-sliced wgemm: next_norm without norm_out");
+    if (epi == EPI_RESID && a.next_norm)
       launch_splitk_combine_norm(a.part_out, p.sp.kc, a.M, a.N, a.ldo, a.resid, a.ldo, a.next_norm, a.eps,
                                  a.norm_out, a.ldo, s);
     else

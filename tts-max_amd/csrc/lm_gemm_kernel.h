@@ -478,12 +478,15 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   // same consume-and-refill loop (no separate drain path) and the ring registers never need
   // path-merging copies (each such copy of an in-flight register is a vmcnt wait, i.e. the
   // ring drained at every unit boundary).
-  const uint32_t wbytes = (uint32_t)((long long)(a.N >> 4) * KT * 1024);  // (< 4 GiB: host-checked)
+  const uint32_t wbytes = (uint32_t)((long long)(a.N >> 4) * KT * 1024);  // (<= kWgemmMaxBytes: launch-checked)
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)wbytes, 0x00020000);
-  // byte offset of this lane's 16 B of stage st of the wave's item of unit uu (NG*KU tiles)
+  // byte offset of this lane's 16 B of stage st of the wave's item of unit uu (NG*KU tiles).
+  // Past the wave's last unit: a sentinel the stage's tile offsets ((g*KU + kk) KiB, added in
+  // uint32) cannot wrap back into the matrix — every piece of the refill stays beyond wbytes
+  constexpr uint32_t kPast = kWgemmSentinel - (uint32_t)(NG * KU - 1) * 1024u;
   auto soff = [&](int uu, int st) -> uint32_t {
     const int ls = cs2 ? ((lane & ~8) | ((min(uu, units - 1) & 1) << 3)) : lane;
-    return uu < units ? (uint32_t)stile(uu, st) * 1024u + (uint32_t)ls * 16u : 0xFFFFFFF0u;
+    return uu < units ? (uint32_t)stile(uu, st) * 1024u + (uint32_t)ls * 16u : kPast;
   };
   // Register ring of R stages (S = stages per item, S % R == 0): the first R stages of the
   // wave's stream are in flight before the prologue runs; consuming a slot refills it with
@@ -950,9 +953,23 @@ inline constexpr Shape3 kShapes[] = {
 inline constexpr int kNumShapes = sizeof(kShapes) / sizeof(kShapes[0]);
 inline bool shape_ng2(int c) { return kShapes[c].ng2; }
 
+// the instantiation a launch runs (the dry run's record; the order of wgemm_kernel's parameters)
+inline std::string wgemm_inst_name(int waves, int ku, int mt, int ng, int ksplit, int asrc, bool norm, int epi, int r,
+                                   bool early, int ksw, bool frows) {
+  char b[128];
+  snprintf(b, sizeof b, "wgemm_kernel<%d, %d, %d, %d, %d, %d, %s, %d, %d, %s, %d, %s>", waves, ku, mt, ng, ksplit, asrc,
+           norm ? "true" : "false", epi, r, early ? "true" : "false", ksw, frows ? "true" : "false");
+  return b;
+}
+
 template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R, bool EARLY>
 static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   const int mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
+  if (dry_launches()) {  // (the branches below, without the launch)
+    const bool frows = mt == 1 && !EARLY && a.fattn_wgs && a.M > 1;
+    dry_record(wgemm_inst_name(WAVES, KU, mt, NG, KSPLIT, ASRC, NORM, EPI, R, mt == 1 && EARLY && !frows, KSPLIT, frows));
+    return;
+  }
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
   lds += (size_t)wgemm_red_floats(WAVES, KSPLIT, NG, mt, a.M, a.K) * sizeof(float);
   if (a.fattn_wgs) {  // QKV + fused decode attention (1..16 rows, D 64 / 128, 16-wave workgroups)
@@ -993,6 +1010,8 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
     }
   }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
+  if ((unsigned long long)a.N * (unsigned long long)(a.sliced ? (size_t)a.K * a.kc : (size_t)a.K) * 2ull > kWgemmMaxBytes)
+    throw std::runtime_error("wgemm: tiled weight matrix above the 32-bit buffer range");
   if (ASRC == A_LDS && !EARLY && a.K % 512 != 0)
     throw std::runtime_error("wgemm: the LDS-DMA prologue needs K a multiple of 512 (plan_wgemm: A_GLOBAL)");
   const dim3 g(grid, a.sliced ? a.kc : 1);

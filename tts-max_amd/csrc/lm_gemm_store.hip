@@ -11,6 +11,7 @@ void launch_wgemm_store(const WgemmArgs& a, const WgemmPlan& p, bool norm, hipSt
 
 void launch_wgemm_kslice(const WgemmArgs& a_in, int units, hipStream_t s) {
   WgemmArgs a = a_in;
+  if (dry_record(wgemm_inst_name(8, 2, 2, 1, 16, A_LDS, false, EPI_STORE, 2, false, 4, false))) return;
   if (a.M < 1 || a.M > 32 || a.K % 512 != 0 || a.kc != 1 || !a.part_out)
     throw std::runtime_error("wgemm kslice: 1..32 rows, K / 4 a multiple of 512, kc 1, partial workspace");
   a.sliced = 0;

@@ -4,7 +4,22 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
 namespace tts {
+
+// Dry run (tts_debug_step_plan): while a recorder is set on this thread, the SpeechLM
+// launchers append what they would launch — the wgemm_kernel template arguments, other
+// kernels by name — and return without any HIP call, so a decode step's launch list can be
+// read on a machine without a GPU (the spill gate, tests/test_kernel_resources.py).
+std::vector<std::string>*& dry_launches();
+inline bool dry_record(const std::string& what) {
+  std::vector<std::string>* v = dry_launches();
+  if (!v) return false;
+  v->push_back(what);
+  return true;
+}
 
 typedef uint16_t bf16_t;
 
@@ -58,11 +73,6 @@ struct AttnArgs {
   const int4* blocks = nullptr;  // prefill: query blocks {first row, rows (<= 16), slot, first position}
   int nblocks = 0;
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS)
-  // batched decode (rows > 1): the context of each (row, kv head) split into `splits` chunks
-  // over as many workgroups (flash-decoding partials in `part`, merged by a second kernel);
-  // splits <= 1: one workgroup per (row, kv head)
-  int splits = 0;
-  float* part = nullptr;  // [rows][KVH][splits][2*4 + 4*D] fp32
   // decode: q | k | v as fp32 partials of a K-sliced QKV launch ([qkv_nsl][rows][ld_qkv], summed
   // in slice order and rounded to bf16 here, as splitk_combine_kernel would) instead of qkv
   const float* qkv_part = nullptr;
@@ -87,6 +97,12 @@ struct StepState {
   int eos_id;
   int min_new;
 };
+
+// Largest tiled weight matrix a wgemm launch streams: one buffer resource with 32-bit byte
+// offsets, and the past-the-last-unit sentinel offsets (wgemm_kernel: kWgemmSentinel - the
+// stage's tile offsets, at most 15 KiB below it) must stay beyond the matrix
+constexpr unsigned long long kWgemmMaxBytes = 0xFFFF0000ull;
+constexpr uint32_t kWgemmSentinel = 0xFFFFFFF0u;
 
 struct WgemmArgs {
   const bf16_t* x = nullptr;  // A: [M][ldx] bf16 activations

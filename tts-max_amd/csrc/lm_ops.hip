@@ -81,6 +81,7 @@ __global__ __launch_bounds__(256) void rmsnorm_reg_kernel(const bf16_t* __restri
 
 void launch_rmsnorm(const bf16_t* x, int ldx, const bf16_t* w, float eps, bf16_t* y, int ldy,
                     int M, int K, hipStream_t s) {
+  if (dry_record("rmsnorm")) return;
   if (K % 8 == 0 && K <= 2048)
     hipLaunchKernelGGL((rmsnorm_reg_kernel<1>), dim3(M), dim3(256), 0, s, x, ldx, w, eps, y, ldy, K);
   else if (K % 8 == 0 && K <= 4096)
@@ -131,6 +132,7 @@ __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* 
 void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
                             int nparts, StepState st, int B, const bf16_t* embed, bf16_t* x,
                             int hidden, hipStream_t s) {
+  if (dry_record("finalize_greedy_kernel")) return;
   hipLaunchKernelGGL(finalize_greedy_kernel, dim3(B), dim3(256), 0, s, part_val, part_idx,
                      part_stride, nparts, st, embed, x, hidden);
 }
@@ -328,6 +330,7 @@ __global__ __launch_bounds__(256) void splitk_combine_norm_fixed_kernel(
 void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp, bf16_t* resid, int ldo,
                                 const bf16_t* normw, float eps, bf16_t* xn, int ldn, hipStream_t s) {
   static const bool fixed = !(getenv("TTS_COMBINE_FIXED") && !atoi(getenv("TTS_COMBINE_FIXED")));
+  if (dry_record("splitk_combine_norm")) return;
   if (fixed && N == 2048 && kc == 4)
     hipLaunchKernelGGL((splitk_combine_norm_fixed_kernel<4, 1>), dim3(M), dim3(256), 0, s, part, M, ldp, resid, ldo,
                        normw, eps, xn, ldn);
@@ -341,6 +344,7 @@ void launch_splitk_combine_norm(const float* part, int kc, int M, int N, int ldp
 
 void launch_splitk_combine(const float* part, int kc, int M, int N, int ldp, bf16_t* out,
                            bf16_t* resid, int ldo, hipStream_t s) {
+  if (dry_record("splitk_combine")) return;
   const int n = M * (N / 8);
   hipLaunchKernelGGL(splitk_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, kc, M, N, ldp,
                      out, resid, ldo);

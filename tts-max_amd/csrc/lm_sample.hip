@@ -197,6 +197,7 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
 }  // namespace
 
 void launch_sample(const SampleArgs& a, int B, hipStream_t s) {
+  if (dry_record("sample_kernel")) return;
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(SMP_THREADS), 0, s, a);
 }
 

@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "tts_synth_fill",
     "tts_op_retile",
     "tts_op_wgemm",
+    "tts_debug_step_plan",
     "tts_op_pgemm",
     "tts_op_sample",
     "tts_op_rmsnorm",
@@ -188,6 +189,7 @@ def load_library() -> ctypes.CDLL:
         "tts_op_sample": (I32, [P, I32, I32, F32, I32, F32, ctypes.c_uint64, I32, P, I32, P, P, P]),
         "tts_op_rmsnorm": (I32, [P, P, F32, P, I32, I32, P]),
         "tts_op_gemm_f32": (I32, [P, I32, I32, I32, P, I32, P, P, I32, P, I32, P]),
+        "tts_debug_step_plan": (I32, [ctypes.POINTER(LmConfig), I32, I32, ctypes.c_char_p, I32]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("TTS_LIB_PATH") and not hasattr(lib, name):

@@ -68,6 +68,29 @@ class RequestOutput:
     outputs: list[CompletionOutput]
 
 
+def lm_config(arch: configs.LmArch, max_batch: int = 1, max_seq_len: int = 2048) -> "_lib.LmConfig":
+    """The C ABI's tts_lm_config of an architecture."""
+    return _lib.LmConfig(
+        hidden_size=arch.hidden_size, num_layers=arch.num_layers, num_heads=arch.num_heads,
+        num_kv_heads=arch.num_kv_heads, head_dim=arch.head_dim, intermediate_size=arch.intermediate_size,
+        vocab_size=arch.vocab_size, tie_word_embeddings=int(arch.tie_word_embeddings),
+        rms_norm_eps=arch.rms_norm_eps, rope_theta=arch.rope_theta, rope_llama3=int(arch.rope_llama3),
+        rope_factor=arch.rope_factor, rope_low_freq_factor=arch.rope_low_freq_factor,
+        rope_high_freq_factor=arch.rope_high_freq_factor,
+        rope_original_max_position=arch.rope_original_max_position, max_batch=max_batch,
+        max_seq_len=max_seq_len)
+
+
+def step_plan(arch: configs.LmArch, rows: int, num_cu: int = 256) -> list[str]:
+    """The kernels one decode step over `rows` rows launches (tts_debug_step_plan: the
+    engine's step code in dry-run mode; no GPU needed): unique, in first-seen order."""
+    lib = _lib.load_library()
+    cfg = lm_config(arch, max_batch=max(rows, 1), max_seq_len=2048)
+    buf = ctypes.create_string_buffer(1 << 16)
+    _lib.check(lib.tts_debug_step_plan(ctypes.byref(cfg), rows, num_cu, buf, len(buf)))
+    return [ln for ln in buf.value.decode().splitlines() if ln]
+
+
 class MI355XSpeechLM:
     """One SpeechLM resident on one MI355X (one engine, one stream)."""
 
@@ -85,15 +108,7 @@ class MI355XSpeechLM:
         h = ctypes.c_void_p()
         _lib.check(self._lib.tts_engine_create(device, ctypes.byref(h)))
         self._h = h
-        cfg = _lib.LmConfig(
-            hidden_size=arch.hidden_size, num_layers=arch.num_layers, num_heads=arch.num_heads,
-            num_kv_heads=arch.num_kv_heads, head_dim=arch.head_dim, intermediate_size=arch.intermediate_size,
-            vocab_size=arch.vocab_size, tie_word_embeddings=int(arch.tie_word_embeddings),
-            rms_norm_eps=arch.rms_norm_eps, rope_theta=arch.rope_theta, rope_llama3=int(arch.rope_llama3),
-            rope_factor=arch.rope_factor, rope_low_freq_factor=arch.rope_low_freq_factor,
-            rope_high_freq_factor=arch.rope_high_freq_factor,
-            rope_original_max_position=arch.rope_original_max_position, max_batch=max_batch,
-            max_seq_len=max_seq_len)
+        cfg = lm_config(arch, max_batch, max_seq_len)
         cos, sin = hf_rope_table(arch, max_seq_len)
         tensors = dict(weights)
         tensors["rope.cos"] = cos
