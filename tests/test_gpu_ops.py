@@ -121,8 +121,9 @@ def test_wgemm_norm_k_not_multiple_of_512(lib, M):
     ref = lm_oracle.linear(lm_oracle.rmsnorm(x, nw, 1e-5), w)
     wt = _tiled(lib, w.cuda())
     out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-    _check(lib.tts_op_wgemm(x.cuda().data_ptr(), M, K, K, wt.data_ptr(), N, nw.cuda().data_ptr(), 1e-5,
-                            out.data_ptr(), N, None, 0, None))
+    xd, nd = x.cuda(), nw.cuda()  # (held: a temporary's block could be reused by the next one)
+    _check(lib.tts_op_wgemm(xd.data_ptr(), M, K, K, wt.data_ptr(), N, nd.data_ptr(), 1e-5, out.data_ptr(), N, None, 0,
+                            None))
     torch.cuda.synchronize()
     _bf16_close(out.cpu(), ref, max_ulps=3, frac=0.03)
     assert torch.equal(out[0].cpu(), out[-1].cpu())

@@ -34,9 +34,9 @@ arch = configs.LM_ARCHS[sys.argv[2]]
 rows_list = [int(r) for r in sys.argv[3].split(",")]
 vocab = configs.vocab_for(arch)
 m = MI355XSpeechLM.synthetic(arch, seed=0x5EED, max_batch=max(rows_list), max_seq_len=320)
-rng = np.random.default_rng(11)
 out = {}
 for rows in rows_list:
+    rng = np.random.default_rng(11 + rows)  # (per row count: a child may run any subset)
     seqs = [synth.synthetic_prompt(vocab, 40 + u, 39, 150 + 3 * u) for u in range(rows)]
     n_last = 6
     gi = rng.integers(0, arch.vocab_size, size=(rows, n_last, 48)).astype(np.int32)
@@ -62,6 +62,8 @@ CASES = [
     ("TTS_COMBINE_FIXED=0", "tts1", "24"),
     ("TTS_SLICED_GRID=0", "tts1", "24"),
     ("TTS_HEAD_GRID=512", "tts1", "1,24"),
+    ("TTS_NORM_ONCE=0", "tts1", "8,16,24"),
+    ("TTS_NORM_ONCE=0", "tts1-max-2l", "8"),
     ("TTS_BALANCE=0", "tts1-max-2l", "8"),
     ("TTS_FUSED_OPROJ_ROWS=0", "tts1-max-2l", "8"),
 ]

@@ -101,6 +101,11 @@ def test_step_plan_lists_the_bench_launches():
     assert "attn_decode_kernel<64>" not in one  # (fused into the QKV launch)
     b32 = step_plan(configs.LM_ARCHS["tts1"], 32)
     assert "attn_decode_kernel<64>" in b32 and "splitk_combine_norm" in b32, b32
+    # 2..16 rows: the attention and o_proj ride the QKV launch (its FROWS instantiation), the
+    # RMSNorms run once per row by the producing launches (gate/up and lm_head without NORM)
+    b8 = step_plan(configs.LM_ARCHS["tts1"], 8)
+    assert "attn_decode_kernel<64>" not in b8 and "rmsnorm" not in b8, b8
+    assert any(k.startswith("wgemm_kernel<8, 2, 1, 2, 4, 1, false, 2,") for k in b8), b8
 
 
 def test_hot_wgemm_instantiations_do_not_spill(spills):

@@ -86,6 +86,8 @@ struct LmWork {
   DevBuf blocks;                                    // prefill query blocks (int4, lm_attn.hip)
   int nblocks = 0;
   DevBuf gran, ferr;                                // fused QKV+attention: granules [QKV/2] u64, error flag
+  DevBuf xgran;                                     // norm-once hand-off: hidden-row granules [2][B][hidden/2] u64
+  DevBuf epoch;                                     // decode-step counter (u32; the hand-off's tags)
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]

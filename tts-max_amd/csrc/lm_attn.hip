@@ -10,7 +10,7 @@
 // absolute position and attends to positions 0..pos of its slot (ragged batching: no
 // padding, each sequence computed as in a batch-1 generate).
 //
-// KV cache of a layer (lm_attn_core.h): K [slot][kv head][S][D], V^T [slot][kv head][D][S] —
+// KV cache of a layer (lm_attn_core.h): K [slot][kv head][S][D], V^T [slot][kv head] in 16 x 32 tiles —
 // the A-operand layouts of S^T = K.Q^T and O^T = V^T.P^T on v_mfma_f32_16x16x32_bf16, so the
 // kernels load every fragment straight into registers.  Both kernels write the attention
 // output (bf16, [rows][H*D]) directly: no chunk partials, no merge pass.
@@ -44,7 +44,7 @@ __global__ void rope_append_kernel(AttnArgs a) {
       a.kcache[(((size_t)slot * a.KVH + h) * a.max_seq + pos) * D + d] = f2bf(rope_at<D>(base + HD + h * D, d, cosr, sinr));
     } else {
       const int j = i - HD - KD, h = j / D, d = j % D;
-      a.vtcache[(((size_t)slot * a.KVH + h) * D + d) * a.max_seq + pos] = base[HD + KD + j];
+      a.vtcache[((size_t)slot * a.KVH + h) * D * a.max_seq + vt_off(a.max_seq, d, pos)] = base[HD + KD + j];
     }
   }
 }
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(dec_nw<D>() * 64) void attn_decode_kernel(AttnArgs 
   // this (slot, kv head))
   if (tid < D) {
     a.kcache[kvbase + (size_t)pos * D + tid] = knew[tid];
-    a.vtcache[kvbase + (size_t)tid * a.max_seq + pos] = vnew[tid];
+    a.vtcache[kvbase + vt_off(a.max_seq, tid, pos)] = vnew[tid];
   }
 }
 
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnArgs a) {
     u32x4_t vf[1][C::DT];
     const int p0 = kb * 32 + 8 * g;
 #pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) vf[0][dt] = *(const u32x4_t*)(vtc + (size_t)(16 * dt + c) * a.max_seq + p0);
+    for (int dt = 0; dt < C::DT; ++dt) vf[0][dt] = *(const u32x4_t*)(vtc + vt_off(a.max_seq, 16 * dt + c, p0));
     f32x4_t s[2];
     scores(kb, s);
     // V elements past the block's last key: zeroed (never-written memory)

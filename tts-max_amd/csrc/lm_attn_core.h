@@ -8,9 +8,13 @@
 // fp32 sum of the unrounded p, o = (P.V) / l rounded to bf16.  The max and the sums are the
 // reference's; only the fp32 summation order differs (products of bf16 operands are exact).
 //
-// KV cache of a layer: K [slot][kv head][S][D] (rows), V^T [slot][kv head][D][S] (columns),
-// S = the position stride (a multiple of 64).  Both are the MFMA operand layouts below, so
-// every fragment is ONE 16-byte load straight from HBM / L2 into registers (no LDS staging).
+// KV cache of a layer: K [slot][kv head][S][D] (rows), V^T [slot][kv head] as tiles of 16
+// dimensions x 32 positions (vt_off below), S = the position stride (a multiple of 64).  Both
+// are the MFMA operand layouts below, so every fragment is ONE 16-byte load straight from HBM /
+// L2 into registers (no LDS staging), and a wave's V^T fragment of one dimension tile is one
+// contiguous KiB — eight whole 128-B lines (round 6: with V^T as plain [D][S] columns a head-dim
+// 128 wave, 32 positions per pass, read half of each 128-B line and its neighbour wave the
+// other half).
 //
 // Work split: NW waves; wave w owns positions base = (pass * NW + w) * PW .. + PW - 1 of each
 // pass.  Per wave and pass:
@@ -46,6 +50,12 @@ constexpr int DEC_NW = 16;
 template <int D> constexpr int dec_nw() { return 16; }
 template <int D> constexpr int dec_pw() { return D == 64 ? 64 : 32; }
 
+// element (d, p) of a (slot, kv head) V^T block: tile (d / 16, p / 32) of 16 x 32 bf16, the 32
+// positions of each dimension contiguous
+TTS_DEV int vt_off(int S, int d, int p) {
+  return (((d >> 4) * (S >> 5) + (p >> 5)) * 16 + (d & 15)) * 32 + (p & 31);
+}
+
 // position of A row `row` of m-tile mt (see pi above)
 TTS_DEV int dec_pos(int base, int mt, int row) {
   return base + 32 * (mt >> 1) + 8 * (row >> 2) + 4 * (mt & 1) + (row & 3);
@@ -78,11 +88,12 @@ TTS_DEV void dec_load_v(const bf16_t* vtc, int S, int base, int lane,
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int ps = 0; ps < C::PS; ++ps) {
-    const int p0 = min(base + 32 * ps + 8 * g, S - 8);
+    // (position blocks past the stride: clamped to the last one; those positions are masked)
+    const int pb = min((base >> 5) + ps, (S >> 5) - 1);
+    const int o0 = (pb * 16 + c) * 32 + 8 * g;  // (vt_off of (16 dt + c, 32 pb + 8 g) = o0 + 16 S dt)
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
-      vf[ps][dt] = O32 ? *(const u32x4_t*)(vtc + ((16 * dt + c) * S + p0))
-                       : *(const u32x4_t*)(vtc + (size_t)(16 * dt + c) * S + p0);
+      vf[ps][dt] = O32 ? *(const u32x4_t*)(vtc + (o0 + dt * 16 * S)) : *(const u32x4_t*)(vtc + o0 + (size_t)dt * 16 * S);
   }
 }
 

@@ -252,6 +252,11 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.gran.alloc((size_t)std::max(B, 2) * (QKV + H * D) / 2 * 8);  // q|k|v, then attention rows
   HIP_CHECK(hipMemsetAsync(w.gran.p, 0xff, w.gran.bytes, s));  // tag 0xffffffff: never a launch's
   w.ferr.alloc(256);
+  // norm-once hand-off granules: two regions of [B][hidden / 2]
+  w.xgran.alloc((size_t)2 * B * (HID / 2) * 8);
+  HIP_CHECK(hipMemsetAsync(w.xgran.p, 0xff, w.xgran.bytes, s));
+  w.epoch.alloc(64);
+  HIP_CHECK(hipMemsetAsync(w.epoch.p, 0, 64, s));
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
   w.kpart.alloc(kpart_bytes(c));
   w.slogits.alloc((size_t)B * V * 4);
@@ -324,6 +329,14 @@ bool use_fused_oproj_rows() {
   return v;
 }
 
+// 17..32 rows: the RMSNorm in the consuming GEMM's LDS prologue (every workgroup normalises
+// the rows it stages) instead of a standalone pass — A/B switch TTS_NORM_PROLOGUE32=1 (the same
+// canonical sum order: the same bits)
+bool norm_prologue32() {
+  static const bool v = getenv("TTS_NORM_PROLOGUE32") && atoi(getenv("TTS_NORM_PROLOGUE32"));
+  return v;
+}
+
 struct Ctx {
   Engine* e;
   hipStream_t s;
@@ -338,6 +351,36 @@ struct Ctx {
   // w.xn holds RMSNorm(w.x, pending_norm) when a residual combine produced it (17..32-row
   // decode: the down projection's K-sliced combine normalises with the next norm weight)
   const bf16_t* pending_norm = nullptr;
+  // a decode step's layers are being issued, and the current layer (the norm-once hand-off's
+  // granule tags: (step << 6) | layer)
+  bool decoding = false;
+  int cur_layer = 0;
+  int nrm_region = 1;  // (the residual launch being issued: 0 = o_proj, 1 = down)
+  // RMSNorm once per row by the producing launch (2..32 decode rows), TTS_NORM_ONCE: 0 = every
+  // consuming workgroup normalises in its prologue; 1 = norm workgroups appended to the fused
+  // QKV + attention + o_proj launch and to the down projection (WgemmArgs::nrm_wgs), and the
+  // K-sliced down projection's combine normalising; 2 (default) = the same without the norm
+  // workgroups on the down launch (measured: 8 rows 755 -> 835 us with them, r6c)
+  int norm_once_mode() const {
+    static const int mode = getenv("TTS_NORM_ONCE") ? atoi(getenv("TTS_NORM_ONCE")) : 2;
+    return mode;
+  }
+  bool norm_once_ok(int rows) const {
+    return norm_once_mode() > 0 && rows >= 2 && rows <= 32 && c.hidden_size % 512 == 0 && c.hidden_size <= 8192;
+  }
+  // the two granule regions of w.xgran ([cap_batch][hidden / 2] each): 0 = the fused o_proj's
+  // rows, 1 = the down projection's (consecutive writers of one region differ in (pos, layer))
+  size_t xgran_region(int r) const { return (size_t)r * w.cap_batch * (c.hidden_size / 2); }
+  void set_norm_wgs(WgemmArgs& a, int rows, const bf16_t* normw, uint64_t* gran, int hid) const {
+    a.nrm_wgs = rows;
+    a.nw_w = normw;
+    a.nw_out = w.xn.as<bf16_t>();
+    a.nw_gran = gran;
+    a.nw_epoch = w.epoch.as<uint32_t>();
+    a.nw_layer = cur_layer;
+    a.nw_hid = hid;
+    a.eps = c.rms_norm_eps;
+  }
   // 17..32-row decode: the K-sliced QKV launch leaves fp32 partials in w.kpart and the decode
   // attention sums them (no combine launch); set by layers() around the QKV gemm
   bool defer_qkv_combine = false, qkv_part_pending = false;
@@ -379,10 +422,10 @@ struct Ctx {
       // pass (same canonical order: identical bits) is cheaper, or none when the producer
       // already wrote the normalised rows
       // (by the batch's row count: every chunk of a 33..64-row batch takes the same path)
-      if (norm && rows > 16 && normw == ready && x == w.x.as<bf16_t>()) {
+      if (norm && normw == ready && x == w.x.as<bf16_t>()) {
         xin = w.xn.as<bf16_t>() + (size_t)r0 * K;
         norm = false;
-      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || rows > 16)) {
+      } else if (norm && (!p.a_lds || p.sliced || K > 4096 || (rows > 16 && !norm_prologue32()))) {
         launch_rmsnorm(xin, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, m, K, s);
         xin = w.xn.as<bf16_t>();
         norm = false;
@@ -434,13 +477,19 @@ struct Ctx {
       a.out = out ? out + (size_t)r0 * ldo : nullptr; a.ldo = ldo;
       a.resid = resid ? resid + (size_t)r0 * ldo : nullptr;
       if (p.sliced) a.part_out = w.kpart.as<float>();
-      const bool fuse_norm = p.sliced && epi == EPI_RESID && next_norm && m > 16 && rows <= 32 && N <= 8192;
+      // the next RMSNorm once per row: in the K-sliced launch's combine (the combine is per row),
+      // or (unsliced residual launches, 2..32 rows) by norm workgroups appended to the launch
+      const bool fuse_norm = p.sliced && epi == EPI_RESID && next_norm && (m > 16 || norm_once_ok(rows)) &&
+                             rows <= 32 && N <= 8192;
       if (fuse_norm) {
         a.next_norm = next_norm;
         a.norm_out = w.xn.as<bf16_t>() + (size_t)r0 * ldo;
       }
+      const bool nrm = !p.sliced && epi == EPI_RESID && next_norm && norm_once_ok(rows) && decoding && rows == m &&
+                       (norm_once_mode() == 1 || nrm_region == 0);
+      if (nrm) set_norm_wgs(a, m, next_norm, w.xgran.as<uint64_t>() + xgran_region(nrm_region), N);
       launch_wgemm(a, p, epi, norm, s);
-      if (fuse_norm) pending_norm = next_norm;
+      if (fuse_norm || nrm) pending_norm = next_norm;
     }
   }
 
@@ -472,11 +521,14 @@ struct Ctx {
   bool fused_attn_ok(int rows, bool decode) const {
     if (!decode || !use_fused_attn() || c.num_layers < 2 || c.num_layers > 64) return false;
     if (rows == 1) return c.head_dim == 64 && wgemm_fattn_ok(QKV(), c.hidden_size, e->num_cu);
-    // 2..16 rows (TTS_FATTN_ROWS = the largest batch that fuses; 0: none): any head dim, the
-    // attention workgroups after the projection's (deadlock-free order), no fused o_proj
+    // 2..16 rows by default (TTS_FATTN_ROWS = the largest batch that fuses; 0: none; up to 32:
+    // at 17..32 rows two m-tiles, the rows staged pre-normalised by the previous down
+    // projection's combine — measured slower than the K-sliced seven-launch layer, round 6:
+    // 32 rows 978 -> 1,041 us, profiles/r6b_ab_frows32.txt): the attention workgroups after the
+    // projection's (deadlock-free order)
     static const int max_rows = getenv("TTS_FATTN_ROWS") ? atoi(getenv("TTS_FATTN_ROWS")) : 16;
     static const bool first = getenv("TTS_FATTN_FIRST") && atoi(getenv("TTS_FATTN_FIRST"));
-    return rows <= std::min(16, max_rows) && !first && wgemm_fattn_rows_ok(rows, QKV(), c.hidden_size, c.head_dim, e->num_cu);
+    return rows <= std::min(32, max_rows) && !first && wgemm_fattn_rows_ok(rows, QKV(), c.hidden_size, c.head_dim, e->num_cu);
   }
   WgemmArgs fused_attn_args(const AttnArgs& a, int layer, bool with_oproj = false) {
     WgemmArgs fx;
@@ -517,11 +569,11 @@ struct Ctx {
            pq.sp.waves == 16 && pq.sp.ku == 2 && pq.sp.ksplit == 16;
   }
 
-  // 2..16 rows: o_proj can ride the fused QKV + attention launch when its stream plan has the
+  // 2..32 rows: o_proj can ride the fused QKV + attention launch when its stream plan has the
   // launch's shape (16 waves, the QKV plan's stage width, K split 16 ways, the item = the
   // two-stage ring) and o_proj's K is the hidden size (its A rows fit the launch's LDS rows)
   bool fused_oproj_rows_ok(int rows) const {
-    if (!use_fused_oproj() || !use_fused_oproj_rows() || rows < 2 || rows > 16) return false;
+    if (!use_fused_oproj() || !use_fused_oproj_rows() || rows < 2 || rows > 32) return false;
     const int HD = c.num_heads * c.head_dim, HID = c.hidden_size;
     const WgemmPlan pq = plan_wgemm(rows, QKV(), HID, EPI_STORE, e->num_cu);
     const WgemmPlan po = plan_wgemm(rows, HID, HD, EPI_RESID, e->num_cu);
@@ -537,13 +589,19 @@ struct Ctx {
     const int HID = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
     const bool fattn = fused_attn_ok(rows, decode);
     const bool foproj = fattn && (rows == 1 ? fused_oproj_ok() : fused_oproj_rows_ok(rows));
+    decoding = decode;
     for (int l = 0; l < c.num_layers; ++l) {
       const LmLayer& ly = M.layers[l];
+      cur_layer = l;
       AttnArgs a = attn_args(l, rows, slot, pos, decode);
       if (fattn) {
-        const WgemmArgs fx = fused_attn_args(a, l, foproj);
+        WgemmArgs fx = fused_attn_args(a, l, foproj);
+        // (2..32 rows, o_proj fused: the ln2 RMSNorm once per row by appended workgroups)
+        const bool nrm = foproj && rows > 1 && norm_once_ok(rows);
+        if (nrm) set_norm_wgs(fx, rows, ly.ln2, w.xgran.as<uint64_t>() + xgran_region(0), HID);
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE, &fx);
+        if (nrm) pending_norm = ly.ln2;
       } else {
         // (defer: TTS_QKV_DEFER=0 keeps the combine launch)
         defer_qkv_combine = decode && rows > 16 && rows <= 32 && use_qkv_defer();
@@ -563,12 +621,14 @@ struct Ctx {
         launch_rope_append(a, s);
         launch_attn_prefill(a, s);
       }
+      nrm_region = 0;
       if (!foproj)  // (decode: o_proj's combine may normalise with ln2 for the gate/up launch)
         gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID,
              nullptr, decode ? ly.ln2 : nullptr);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
+      nrm_region = 1;
       gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),
            EPI_RESID, nullptr, decode ? next_norm : nullptr);
     }
@@ -588,6 +648,7 @@ struct Ctx {
     st.seen_stride = c.vocab_size / 32 + 1;
     st.counts = nullptr;
     st.row_seed = w.row_seed.as<unsigned long long>();
+    st.epoch = w.epoch.as<uint32_t>();
     st.out_ids = w.out_ids.as<int>();
     st.out_stride = w.out_cap;
     st.eos_id = eos;
@@ -660,6 +721,7 @@ static void prefill_rows_setup(Ctx& X, const int32_t* ids, const int32_t* lens, 
   // (with a matching tag the attention workgroups could read them before this step's QKV
   // workgroups overwrite them)
   HIP_CHECK(hipMemsetAsync(X.w.gran.p, 0xff, X.w.gran.bytes, X.s));
+  HIP_CHECK(hipMemsetAsync(X.w.xgran.p, 0xff, X.w.xgran.bytes, X.s));
 }
 
 // The decode step (all layers + lm_head + pick + finalize over B rows) captured once into a
@@ -1246,6 +1308,7 @@ void lm_score_decode(Engine* e, const int32_t* ids, const int32_t* lens, int B, 
     launch_embed(e->w.row_idx.as<int>(), X.M.embed_rows.as<bf16_t>(), e->w.x.as<bf16_t>(), B, HID, s);
     X.layers(B, e->w.row_slot.as<int>(), e->w.row_pos.as<int>(), true);
     X.gemm(e->w.x.as<bf16_t>(), B, HID, X.M.lm_head, V, X.M.final_norm, lg.as<bf16_t>(), V, nullptr, EPI_STORE);
+    launch_bump_epoch(e->w.epoch.as<uint32_t>(), s);  // (a decode step without the finalize kernel)
     check_launch();
     HIP_CHECK(hipMemcpyAsync(h.data(), lg.p, h.size() * 2, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));  // (h and the token/position vectors are reused)

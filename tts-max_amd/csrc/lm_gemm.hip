@@ -197,14 +197,14 @@ bool wgemm_fattn_ok(int N, int K, int num_cu) {
   return kch % 64 == 0 && (kch + NT - 1) / NT <= ea;
 }
 
-// 2..16 rows: the QKV launch of the batched step can carry the attention when it is one
-// 16-wave, unsliced launch with the A rows in LDS (any prologue)
+// 2..32 rows: the QKV launch of the batched step can carry the attention when it is one
+// 16-wave, unsliced launch with the A rows in LDS (any prologue; 17..32 rows: two m-tiles)
 bool wgemm_fattn_rows_ok(int M, int N, int K, int D, int num_cu) {
   const WgemmPlan p = plan_wgemm(M, N, K, EPI_STORE, num_cu);
   // (launch_wgemm runs the fused launch with whole units, csplit 1; the launch shape's ring
   // depth is 2 when the item's stage count is even, which the fused o_proj also requires)
   const int S = (K / 32) / (p.sp.ksplit * p.sp.ku);
-  return M >= 2 && M <= 16 && p.a_lds && !p.sliced && p.sp.waves == DEC_NW && D == wgemm_fattn_d(p.sp.ku) &&
+  return M >= 2 && M <= 32 && p.a_lds && !p.sliced && p.sp.waves == DEC_NW && D == wgemm_fattn_d(p.sp.ku) &&
          K % 512 == 0 && S % 2 == 0;
 }
 

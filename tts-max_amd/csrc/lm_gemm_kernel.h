@@ -58,6 +58,19 @@ TTS_DEV bool fattn_wait(Poll ready, int* err, int spins, bool report) {
   return true;
 }
 
+// The residual epilogue's half of the hand-off: lane holds the updated bf16 value of column n
+// of row m (rows differ by lane group only, so a lane and its neighbour lane ^ 1 hold the same
+// row's columns n and n ^ 1); even lanes publish the pair {tag, (n + 1, n)} with one agent-scope
+// 8-byte store.  Called by every lane of the wave (the shuffle); `pub` = this lane's value is a
+// real output (row < M, the lane's column half)
+TTS_DEV void publish_pair(uint64_t* gran_row, int n, bf16_t val, uint32_t tag, bool pub) {
+  const uint32_t mine = (uint32_t)val;
+  const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+  if (pub && !(n & 1))
+    __hip_atomic_store(gran_row + (n >> 1), ((uint64_t)tag << 32) | (other << 16) | mine, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NT, int D>
 TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   static_assert(NT == DEC_NW * 64, "the fused attention runs on 16-wave workgroups");
@@ -125,7 +138,7 @@ TTS_DEV void fattn_consumer(const WgemmArgs& wa, char* smem, int b) {
   // the new position's roped k and v to the cache, after this workgroup's reads
   if (tid < D) {
     a.kcache[kvbase + (size_t)pos * D + tid] = knew[tid];
-    a.vtcache[kvbase + (size_t)tid * a.max_seq + pos] = vnew[tid];
+    a.vtcache[kvbase + vt_off(a.max_seq, tid, pos)] = vnew[tid];
   }
 }
 
@@ -189,13 +202,14 @@ TTS_DEV void fused_oproj(const WgemmArgs& a, bf16_t* xs, float* red, int wave, i
   }
 }
 
-// The same for the 2..16-row QKV launch (FROWS, order 0): o_proj unit u on its own workgroup.
+// The same for the 2..32-row QKV launch (FROWS, order 0): o_proj unit u on its own workgroup.
 // Each wave's K range of the o_proj plan (the launch's shape: KSPLIT == WAVES, R stages = the
 // item, fo_kc K chunks) comes from the attention rows' granules (gran + M*N/2: row m's
 // H*D/2 granules, tag = that row's (pos, layer)), R*KU/4 per lane and row, staged into the
 // wave's own columns of the LDS rows (read back by this wave only), then the o_proj launch's
-// MFMAs (rows clamped to M - 1 as its m-tile does), split-K order and residual epilogue.
-template <int KU, int KSPLIT, int R>
+// MFMAs over MT 16-row m-tiles (rows clamped to M - 1 as its m-tiles do), split-K order and
+// residual epilogue.
+template <int KU, int KSPLIT, int R, int MT>
 TTS_DEV void fused_oproj_rows(const WgemmArgs& a, bf16_t* xs, float* red, int wave, int lane, int u) {
   const int M = a.M, HD = a.fa.H * a.fa.D, ldxs = HD + 8, hid = a.fo_units * 16;
   unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
@@ -214,9 +228,11 @@ TTS_DEV void fused_oproj_rows(const WgemmArgs& a, bf16_t* xs, float* red, int wa
     for (int kk = 0; kk < KU; ++kk)
       wr[st][kk] = __builtin_nontemporal_load((const u32x4_t*)a.fo_w +
                                               ((((long long)st * nr + u) * KSPLIT + kpart) * KU + kk) * 64 + lane);
-  bf16_t rr[4];
+  bf16_t rr[MT][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) rr[r] = a.fo_resid[(size_t)min(4 * (lane >> 4) + r, M - 1) * hid + u * 16 + (lane & 15)];
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rr[mt][r] = a.fo_resid[(size_t)min(mt * 16 + 4 * (lane >> 4) + r, M - 1) * hid + u * 16 + (lane & 15)];
   constexpr int NGL = R * KU >= 4 ? R * KU / 4 : 1;  // granules per lane and row (R*KU k-tiles of 16; host: R*KU % 4 == 0)
   int col[NGL];
 #pragma unroll
@@ -256,36 +272,106 @@ TTS_DEV void fused_oproj_rows(const WgemmArgs& a, bf16_t* xs, float* red, int wa
   }
   TTS_STAMP(stp, 2);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  const bf16_t* xr = xs + (size_t)min(lane & 15, M - 1) * ldxs + 8 * (lane >> 4);
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int st = 0; st < R; ++st)
 #pragma unroll
-    for (int kk = 0; kk < KU; ++kk) {
-      const u32x4_t av = *(const u32x4_t*)(xr + ktile(st, kk) * 32);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av), as_bf16x8(wr[st][kk]), acc, 0, 0, 0);
-    }
-  if (kpart > 0) *(f32x4_t*)(red + ((size_t)(kpart - 1) * 64 + lane) * 4) = acc;
+    for (int kk = 0; kk < KU; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16_t* xr = xs + (size_t)min(mt * 16 + (lane & 15), M - 1) * ldxs + 8 * (lane >> 4);
+        const u32x4_t av = *(const u32x4_t*)(xr + ktile(st, kk) * 32);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av), as_bf16x8(wr[st][kk]), acc[mt], 0, 0, 0);
+      }
+  // split-K combine (as the GEMM kernel's: 16-B partials, p ascending; slot (p - 1, mt))
+  if (kpart > 0) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) *(f32x4_t*)(red + (((size_t)(kpart - 1) * MT + mt) * 64 + lane) * 4) = acc[mt];
+  }
   lds_barrier();
   if (kpart == 0) {
-    constexpr int HB = 8;
+    constexpr int HB = 8 / MT;
 #pragma unroll
     for (int p0 = 1; p0 < KSPLIT; p0 += HB) {
-      f32x4_t pv[HB];
+      f32x4_t pv[HB][MT];
 #pragma unroll
       for (int j = 0; j < HB; ++j)
-        if (p0 + j < KSPLIT) pv[j] = *(const f32x4_t*)(red + ((size_t)(p0 + j - 1) * 64 + lane) * 4);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          if (p0 + j < KSPLIT) pv[j][mt] = *(const f32x4_t*)(red + (((size_t)(p0 + j - 1) * MT + mt) * 64 + lane) * 4);
 #pragma unroll
       for (int j = 0; j < HB; ++j)
-        if (p0 + j < KSPLIT) acc += pv[j];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          if (p0 + j < KSPLIT) acc[mt] += pv[j][mt];
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = 4 * (lane >> 4) + r;
-      if (m < M) a.fo_resid[(size_t)m * hid + u * 16 + (lane & 15)] = f2bf(bf2f(rr[r]) + rbf(acc[r]));
-    }
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mt * 16 + 4 * (lane >> 4) + r;
+        const bf16_t ob = f2bf(bf2f(rr[mt][r]) + rbf(acc[mt][r]));
+        if (m < M) a.fo_resid[(size_t)m * hid + u * 16 + (lane & 15)] = ob;
+        if (a.nrm_wgs)  // (wave-uniform)
+          publish_pair(a.nw_gran + (size_t)min(m, M - 1) * (hid / 2), u * 16 + (lane & 15), ob,
+                       (*a.nw_epoch << 6) | (uint32_t)a.nw_layer, m < M);
+      }
   }
   TTS_STAMP(stp, 3);
+}
+
+// ------------------------------------------------------------ RMSNorm once per row -----
+// Appended workgroup `row` of a launch whose residual epilogue publishes the updated hidden
+// rows as granules (WgemmArgs::nrm_wgs): gathers the row into LDS once every pair carries this
+// launch's tag, then the standalone rmsnorm_kernel's arithmetic — a wave per 512-value segment
+// (chunk_sumsq + the wave DPP tree), the segments summed in order, every product rounded as in
+// every other RMSNorm path — and writes the normalised row to nw_out.
+template <int NT>
+TTS_DEV void norm_role(const WgemmArgs& a, char* smem, int row) {
+  const int hid = a.nw_hid, ng = hid / 2, nseg = hid / 512;  // (host: hid % 512 == 0, hid <= 8192)
+  bf16_t* xr = (bf16_t*)smem;
+  float* segs = (float*)(smem + (((size_t)hid * 2 + 15) & ~(size_t)15));
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned long long* stp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
+  TTS_STAMP(stp, 0);
+  const uint32_t tag = (*a.nw_epoch << 6) | (uint32_t)a.nw_layer;
+  const uint64_t* gp = a.nw_gran + (size_t)row * ng;
+  constexpr int GPT = 8192 / 2 / NT > 0 ? 8192 / 2 / NT : 1;  // granules per thread (hid <= 8192)
+  uint64_t v[GPT];
+  fattn_wait([&] {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+      const int i = min(j * NT + tid, ng - 1);
+      v[j] = __hip_atomic_load(gp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = ok && (uint32_t)(v[j] >> 32) == tag;
+    }
+    return ok;
+  }, a.fattn_err, a.fattn_spins, true);
+#pragma unroll
+  for (int j = 0; j < GPT; ++j)
+    if (j * NT + tid < ng) ((uint32_t*)xr)[j * NT + tid] = (uint32_t)v[j];
+  lds_barrier();
+  TTS_STAMP(stp, 1);
+  for (int sg = wave; sg < nseg; sg += NT / 64) {  // canonical order (chunk_sumsq)
+    const float s = wave_sum_dpp(chunk_sumsq(*(const u32x4_t*)(xr + sg * 512 + lane * 8)));
+    if (lane == 0) segs[sg] = s;
+  }
+  lds_barrier();
+  float ss = 0.f;
+  for (int sg = 0; sg < nseg; ++sg) ss += segs[sg];
+  const float r = 1.0f / sqrtf(ss / (float)hid + a.eps);
+  for (int k = tid * 8; k < hid; k += NT * 8) {
+    u32x4_t x = *(const u32x4_t*)(xr + k);
+    const u32x4_t g = *(const u32x4_t*)(a.nw_w + k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = pack_bf2(bf_lo(g[q]) * rbf(bf_lo(x[q]) * r), bf_hi(g[q]) * rbf(bf_hi(x[q]) * r));
+    *(u32x4_t*)(a.nw_out + (size_t)row * hid + k) = x;
+  }
+  TTS_STAMP(stp, 2);
 }
 
 // ---------------------------------------------------------------- the GEMM kernel -----
@@ -307,20 +393,33 @@ constexpr int A_GLOBAL = 0, A_LDS = 1;
 // KSW < KSPLIT (K-sliced over workgroups, kc = 1 layouts): a unit's KSPLIT layout k-parts are
 // spread over SL = KSPLIT / KSW workgroups (grid.y), KSW waves each; a.K = the K / SL columns
 // a workgroup stages, fp32 partials of each slice to part_out (summed by a combine kernel).
-// FROWS: the 2..16-row QKV launch carrying the decode attention (its own instantiation, so the
-// consumer's registers stay out of the plain launches of the same shape)
+// FROWS: the 2..32-row QKV launch carrying the decode attention (its own instantiation, so the
+// consumer's registers stay out of the plain launches of the same shape; MT_MAX 1 or 2)
 template <int WAVES, int KU, int MT_MAX, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, int R,
           bool EARLY, int KSW = KSPLIT, bool FROWS = false>
 __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = WAVES * 64;
   // (one row: the register-staged prologue (EARLY); 2..16 rows (one m-tile): any prologue)
-  constexpr bool FATT = EPI == EPI_STORE && MT_MAX == 1 && ASRC == A_LDS && WAVES == DEC_NW && KSW == KSPLIT &&
-                        ((EARLY && !FROWS) || (!EARLY && FROWS));
+  // (the one-row form carries head dim 64 only, wgemm_fattn_ok: the KU 4 (head dim 128)
+  // register-staged instantiation keeps the consumer's registers out)
+  constexpr bool FATT = EPI == EPI_STORE && ASRC == A_LDS && WAVES == DEC_NW && KSW == KSPLIT &&
+                        ((MT_MAX == 1 && EARLY && !FROWS && wgemm_fattn_d(KU) == 64) ||
+                         (MT_MAX <= 2 && !EARLY && FROWS));
+  // RMSNorm once per row (a.nrm_wgs): the grid's last workgroups (they wait on every other
+  // block: the residual epilogues that publish the rows)
+  constexpr bool NRM = EPI == EPI_RESID || (FATT && FROWS);
+  if constexpr (NRM) {
+    if (a.nrm_wgs && (int)blockIdx.x >= (int)gridDim.x - a.nrm_wgs) {
+      norm_role<NT>(a, smem, (int)blockIdx.x - ((int)gridDim.x - a.nrm_wgs));
+      return;
+    }
+  }
+  const int nrm_wgs = NRM ? a.nrm_wgs : 0;
   // fused launch (a.fattn_wgs): the grid's projection / attention / o_proj workgroups
   // (WgemmArgs::fattn_first for the two orders)
   const int fo_wgs = (FATT && a.fattn_wgs && !a.fattn_first) ? a.fo_units : 0;  // o_proj workgroups (order 0)
-  const int nproj = (int)gridDim.x - (FATT ? a.fattn_wgs : 0) - fo_wgs;
+  const int nproj = (int)gridDim.x - nrm_wgs - (FATT ? a.fattn_wgs : 0) - fo_wgs;
   if constexpr (FATT) {
     if (a.fattn_wgs) {
       const int cb = a.fattn_first ? (int)blockIdx.x : (int)blockIdx.x - nproj;
@@ -333,7 +432,8 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const size_t xs_bytes = (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15);
         if constexpr (FROWS) {
-          fused_oproj_rows<KU, KSPLIT, R>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane, cb - a.fattn_wgs);
+          fused_oproj_rows<KU, KSPLIT, R, MT_MAX>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane,
+                                                  cb - a.fattn_wgs);
         } else {
           const uint32_t tag = ((uint32_t)a.fa.row_pos[0] << 6) | (uint32_t)a.fattn_layer;
           fused_oproj<KU, KSPLIT, R>(a, (bf16_t*)smem, (float*)(smem + xs_bytes), wave, lane, tag, cb - a.fattn_wgs);
@@ -403,7 +503,7 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   constexpr bool FTAGS = FATT && !EARLY;
   int ftag_pos = 0;
   if constexpr (FTAGS) {
-    if (a.fattn_wgs) ftag_pos = a.fa.row_pos[min(lane & 15, M - 1)];
+    if (a.fattn_wgs) ftag_pos = a.fa.row_pos[min(lane & (16 * MT_MAX - 1), M - 1)];
   }
   // (a) A rows (+ RMSNorm weight) for the LDS prologue, EA chunks per thread at most
   constexpr int EA = wgemm_ea(WAVES);
@@ -459,7 +559,9 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {  // (no mt < mtn test: loads behind a branch cost exact vmcnt)
       const int m = min(mt * 16 + 4 * (lane >> 4) + r, M - 1);
-      if constexpr (EPI == EPI_RESID) rre[mt][r] = a.resid[(size_t)m * a.ldo + (u_first >> cs2) * 16 + (lane & 15)];
+      if constexpr (EPI == EPI_RESID) {
+        rre[mt][r] = a.resid[(size_t)m * a.ldo + (u_first >> cs2) * 16 + (lane & 15)];
+      }
       if constexpr (EPI == EPI_LOGITS) {
         eosr[mt][r] = a.eos_mask[m];
         seen_cur[mt][r] = a.seen[(size_t)m * a.seen_stride + (u_first >> 1)];
@@ -673,9 +775,10 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
   TTS_STAMP(stp, 1);
   // (the tags' LDS slots: the last 16 floats of the scratch region's slack; read after the
   // split-K combine's barriers)
-  uint32_t* ftag_lds = (uint32_t*)(red + wgemm_red_floats(WAVES, KSPLIT, NG, MT_MAX, M, a.K) - 16);
+  uint32_t* ftag_lds = (uint32_t*)(red + wgemm_red_floats(WAVES, KSPLIT, NG, MT_MAX, M, a.K) - 32);
   if constexpr (FTAGS) {
-    if (a.fattn_wgs && wave == 0 && lane < 16) ftag_lds[lane] = ((uint32_t)ftag_pos << 6) | (uint32_t)a.fattn_layer;
+    if (a.fattn_wgs && wave == 0 && lane < 16 * MT_MAX)
+      ftag_lds[lane] = ((uint32_t)ftag_pos << 6) | (uint32_t)a.fattn_layer;
   }
 
   // per-lane running argmax (EPI_LOGITS): rows m = mt*16 + 4*(lane>>4) + r
@@ -837,7 +940,12 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             else a.out[m * a.ldo + n] = f2bf(acc[0][mt][r]);
           } else if constexpr (EPI == EPI_RESID) {
             bf16_t* p = a.resid + (m * a.ldo + n);
-            *p = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
+            const bf16_t ob = f2bf(bf2f(first ? rre[mt][r] : *p) + rbf(acc[0][mt][r]));
+            *p = ob;
+            // norm once per row: the pair (n, n ^ 1) of row m as a granule (the neighbour lane
+            // holds the same row's other column and is in this branch with it)
+            if (nrm_wgs)
+              publish_pair(a.nw_gran + (size_t)m * (a.nw_hid / 2), n, ob, (*a.nw_epoch << 6) | (uint32_t)a.nw_layer, true);
           } else if constexpr (EPI == EPI_SWIGLU) {
             // unit u = (gate tile, up tile) pair for intermediate columns u*16 .. u*16+15
             const float gt = rbf(acc[0][mt][r]);
@@ -865,12 +973,14 @@ __global__ __launch_bounds__(WAVES * 64) void wgemm_kernel(WgemmArgs a) {
             const uint64_t g = ((uint64_t)ftag << 32) | (other << 16) | mine;
             __hip_atomic_store(a.gran + n / 2, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
-        } else {  // lane holds rows 4 (lane >> 4) + r of column u * 16 + (lane & 15)
+        } else {  // lane holds rows mt * 16 + 4 (lane >> 4) + r of column u * 16 + (lane & 15)
+#pragma unroll
+          for (int mt = 0; mt < MT_MAX; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t mine = (uint32_t)f2bf(acc[0][0][r]);
+            const uint32_t mine = (uint32_t)f2bf(acc[0][mt][r]);
             const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
-            const int m = 4 * (lane >> 4) + r;
+            const int m = mt * 16 + 4 * (lane >> 4) + r;
             if (!(lane & 1) && m < M) {
               const int n = u * 16 + (lane & 15);
               const uint64_t g = ((uint64_t)ftag_lds[m] << 32) | (other << 16) | mine;
@@ -966,18 +1076,20 @@ template <int WAVES, int KU, int NG, int KSPLIT, int ASRC, bool NORM, int EPI, i
 static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
   const int mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
   if (dry_launches()) {  // (the branches below, without the launch)
-    const bool frows = mt == 1 && !EARLY && a.fattn_wgs && a.M > 1;
+    const bool frows = mt <= 2 && !EARLY && a.fattn_wgs && a.M > 1;
     dry_record(wgemm_inst_name(WAVES, KU, mt, NG, KSPLIT, ASRC, NORM, EPI, R, mt == 1 && EARLY && !frows, KSPLIT, frows));
     return;
   }
   size_t lds = (ASRC != A_GLOBAL) ? (((size_t)a.M * (a.K + 8) * 2 + 15) & ~(size_t)15) : 0;
   lds += (size_t)wgemm_red_floats(WAVES, KSPLIT, NG, mt, a.M, a.K) * sizeof(float);
   if (a.fattn_wgs) {  // QKV + fused decode attention (1..16 rows, D 64 / 128, 16-wave workgroups)
-    if (!(EPI == EPI_STORE && ASRC == A_LDS && a.M >= 1 && a.M <= 16 && a.fa.D == wgemm_fattn_d(KU) &&
+    if (!(EPI == EPI_STORE && ASRC == A_LDS && a.M >= 1 && a.M <= 32 && a.fa.D == wgemm_fattn_d(KU) &&
           WAVES == DEC_NW && a.gran && a.fattn_err && !a.sliced && a.csplit == 1 && a.fattn_wgs == a.M * a.fa.KVH))
-      throw std::runtime_error("wgemm: fused attention needs a 1..16-row 16-wave QKV launch (D 64 or 128)");
+      throw std::runtime_error("wgemm: fused attention needs a 1..32-row 16-wave QKV launch (D 64 or 128)");
     if ((a.M == 1) != EARLY)
       throw std::runtime_error("wgemm: fused attention: one row = the register-staged prologue, 2..16 rows = not");
+    if (a.M == 1 && a.fa.D != 64)
+      throw std::runtime_error("wgemm: fused one-row attention: head dim 64 only");
     if (a.M > 1 && a.fattn_first)
       throw std::runtime_error("wgemm: multi-row fused attention: producer-first grid order only");
     if (a.fo_units && a.M > 1) {  // fused o_proj behind the 2..16-row attention (order 0)
@@ -1009,16 +1121,30 @@ static void launch_one_e(const WgemmArgs& a, int grid, hipStream_t s) {
       if (grid > cus) throw std::runtime_error("wgemm: fused attention grid exceeds one workgroup per CU");
     }
   }
+  if (a.nrm_wgs) {  // RMSNorm once per row: M workgroups appended last (norm_role)
+    const bool producer = EPI == EPI_RESID || (a.fattn_wgs && a.fo_units && a.M > 1 && !EARLY);
+    if (!(producer && a.nrm_wgs == a.M && (EPI != EPI_RESID || a.M <= 16) && a.nw_w && a.nw_out && a.nw_gran && a.nw_epoch && a.nw_hid % 512 == 0 &&
+          a.nw_hid <= 8192 && a.nw_hid == (EPI == EPI_RESID ? a.N : a.fo_units * 16) && !a.sliced &&
+          (WAVES * 64) * (8192 / 2 / (WAVES * 64) > 0 ? 8192 / 2 / (WAVES * 64) : 1) * 2 >= a.nw_hid))
+      throw std::runtime_error("wgemm: norm-once workgroups need a residual launch over hid % 512 == 0 columns");
+    lds = std::max(lds, (((size_t)a.nw_hid * 2 + 15) & ~(size_t)15) + (size_t)(a.nw_hid / 512) * 4 + 64);
+    grid += a.nrm_wgs;
+  }
   if (lds > 160 * 1024) throw std::runtime_error("wgemm: LDS request above 160 KiB");
   if ((unsigned long long)a.N * (unsigned long long)(a.sliced ? (size_t)a.K * a.kc : (size_t)a.K) * 2ull > kWgemmMaxBytes)
     throw std::runtime_error("wgemm: tiled weight matrix above the 32-bit buffer range");
   if (ASRC == A_LDS && !EARLY && a.K % 512 != 0)
     throw std::runtime_error("wgemm: the LDS-DMA prologue needs K a multiple of 512 (plan_wgemm: A_GLOBAL)");
   const dim3 g(grid, a.sliced ? a.kc : 1);
-  if (mt == 1 && !EARLY && a.fattn_wgs && a.M > 1) {
-    if constexpr (EPI == EPI_STORE && ASRC == A_LDS && WAVES == DEC_NW)
-      hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, false, KSPLIT, true>), g,
-                         dim3(WAVES * 64), lds, s, a);
+  if (mt <= 2 && !EARLY && a.fattn_wgs && a.M > 1) {  // (FROWS: 2..32 rows)
+    if constexpr (EPI == EPI_STORE && ASRC == A_LDS && WAVES == DEC_NW) {
+      if (mt == 1)
+        hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, false, KSPLIT, true>), g,
+                           dim3(WAVES * 64), lds, s, a);
+      else
+        hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 2, NG, KSPLIT, ASRC, NORM, EPI, R, false, KSPLIT, true>), g,
+                           dim3(WAVES * 64), lds, s, a);
+    }
   } else if (mt == 1)
     hipLaunchKernelGGL((wgemm_kernel<WAVES, KU, 1, NG, KSPLIT, ASRC, NORM, EPI, R, EARLY>), g,
                        dim3(WAVES * 64), lds, s, a);

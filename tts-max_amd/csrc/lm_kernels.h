@@ -62,7 +62,7 @@ struct AttnArgs {
   const int* row_slot = nullptr;  // KV slot (sequence) of each query row
   const int* row_pos = nullptr;   // absolute position of each query row
   bf16_t* kcache = nullptr;       // this layer's K rows: [slots][KVH][max_seq][D]
-  bf16_t* vtcache = nullptr;      // this layer's V columns: [slots][KVH][D][max_seq]
+  bf16_t* vtcache = nullptr;      // this layer's V^T: [slots][KVH] blocks of D x max_seq in 16 x 32 tiles (vt_off)
   int max_seq = 0;                // position stride of the cache (a multiple of 64)
   const bf16_t* rope_cos = nullptr;  // [max_seq][D]
   const bf16_t* rope_sin = nullptr;
@@ -94,6 +94,7 @@ struct StepState {
   int* n_active;      // [1]
   uint16_t* counts;   // [B][V] new-token counts (frequency penalty) or nullptr
   unsigned long long* row_seed;  // [B] sampling key of each row
+  uint32_t* epoch;    // [1] step counter (+1 by the finalize of every step: the norm-once hand-off's tags)
   int eos_id;
   int min_new;
 };
@@ -161,6 +162,22 @@ struct WgemmArgs {
   const bf16_t* fo_w = nullptr;
   int fo_units = 0, fo_ur = 0, fo_kc = 1;
   bf16_t* fo_resid = nullptr;
+  // RMSNorm once per row, by the producer launch (2..32 decode rows; round 6): the launch's
+  // residual epilogue (fused o_proj of the QKV launch, or the down projection's own) also
+  // publishes every pair of the updated hidden row as a granule {bf16 pair, tag = (step << 6) |
+  // layer} in nw_gran [M][hid / 2], and nrm_wgs = M workgroups appended last in the grid (each
+  // waits only on lower blocks) gather one row each and write RMSNorm(row, nw_w) to nw_out
+  // [M][hid] in the canonical order (chunk_sumsq per 16 B, the wave DPP tree per 512 values,
+  // segments in order): the same bits as every other RMSNorm path.  The consumer launch then
+  // stages normalised rows instead of every workgroup normalising every row.  The step counter
+  // (*nw_epoch, one scalar load: no registers held through the weight stream) advances at every
+  // decode step, so two launches that write one granule region never share a tag.
+  int nrm_wgs = 0;
+  const bf16_t* nw_w = nullptr;
+  bf16_t* nw_out = nullptr;
+  uint64_t* nw_gran = nullptr;
+  const uint32_t* nw_epoch = nullptr;
+  int nw_layer = 0, nw_hid = 0;
   unsigned long long* stamps = nullptr;  // diagnostic build only (TTS_STAMPS): [block][8]
   int csplit = 1;     // 2: each 16-column unit runs as two 8-column halves (twice the workgroups; filled in by launch_wgemm)
   int diag = 0;       // timing diagnostics only (TTS_WGEMM_DIAG): 1 no prologue, 2 no epilogue, 8 barrier before the stream, 64 per-wave norm-end stamps
@@ -257,6 +274,7 @@ struct SampleArgs {
 constexpr int SAMPLE_MAX_TOP_K = 1024;
 void launch_sample(const SampleArgs& a, int B, hipStream_t s);
 
+void launch_bump_epoch(uint32_t* epoch, hipStream_t s);  // *epoch += 1 (a decode step without finalize)
 void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
                             int nparts, StepState st, int B, const bf16_t* embed, bf16_t* x,
                             int hidden, hipStream_t s);

@@ -125,8 +125,19 @@ __global__ void finalize_greedy_kernel(const float* __restrict__ pv, const int* 
                                        int hidden) {
   __shared__ int lds[16];
   const int b = blockIdx.x;
+  // the step counter (norm-once hand-off tags, WgemmArgs::nw_epoch): +1 per step, every step
+  if (b == 0 && threadIdx.x == 0 && st.epoch) __hip_atomic_fetch_add(st.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   finalize_row<256, false>(pv + (size_t)b * part_stride, pi + (size_t)b * part_stride, nparts, st, b, embed, x,
                            hidden, lds);
+}
+
+__global__ void bump_epoch_kernel(uint32_t* epoch) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+void launch_bump_epoch(uint32_t* epoch, hipStream_t s) {
+  if (dry_record("bump_epoch_kernel")) return;
+  hipLaunchKernelGGL(bump_epoch_kernel, dim3(1), dim3(64), 0, s, epoch);
 }
 
 void launch_finalize_greedy(const float* part_val, const int* part_idx, int part_stride,
