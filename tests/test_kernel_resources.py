@@ -102,10 +102,14 @@ def test_step_plan_lists_the_bench_launches():
     b32 = step_plan(configs.LM_ARCHS["tts1"], 32)
     assert "attn_decode_kernel<64>" in b32 and "splitk_combine_norm" in b32, b32
     # 2..16 rows: the attention and o_proj ride the QKV launch (its FROWS instantiation), the
-    # RMSNorms run once per row by the producing launches (gate/up and lm_head without NORM)
+    # RMSNorms run in the consumers' prologues, no standalone norm pass
     b8 = step_plan(configs.LM_ARCHS["tts1"], 8)
     assert "attn_decode_kernel<64>" not in b8 and "rmsnorm" not in b8, b8
-    assert any(k.startswith("wgemm_kernel<8, 2, 1, 2, 4, 1, false, 2,") for k in b8), b8
+    assert any(k.startswith("wgemm_kernel<8, 2, 1, 2, 4, 1, true, 2,") for k in b8), b8
+    # 10..16 rows: the K-sliced down projection's combine normalises each row once for the next
+    # QKV launch (TTS_NORM_ONCE 3), which then stages the rows without its RMSNorm prologue
+    b16 = step_plan(configs.LM_ARCHS["tts1"], 16)
+    assert "splitk_combine_norm" in b16 and "wgemm_kernel<16, 2, 1, 1, 16, 1, false, 0, 2, false, 16, true>" in b16, b16
 
 
 def test_hot_wgemm_instantiations_do_not_spill(spills):

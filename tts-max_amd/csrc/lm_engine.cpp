@@ -359,10 +359,13 @@ struct Ctx {
   // RMSNorm once per row by the producing launch (2..32 decode rows), TTS_NORM_ONCE: 0 = every
   // consuming workgroup normalises in its prologue; 1 = norm workgroups appended to the fused
   // QKV + attention + o_proj launch and to the down projection (WgemmArgs::nrm_wgs), and the
-  // K-sliced down projection's combine normalising; 2 (default) = the same without the norm
-  // workgroups on the down launch (measured: 8 rows 755 -> 835 us with them, r6c)
+  // K-sliced down projection's combine normalising; 2 = the same without the norm workgroups on
+  // the down launch; 3 (default) = only the K-sliced down's combine (a per-row kernel already)
+  // normalises.  The appended norm workgroups were measured slower (their gather after the last
+  // producer costs more than the prologue norm they remove: TTS-1 8 rows 755 -> 835 / 801 us
+  // with modes 1 / 2, TTS-1-Max 8 rows 3,096 -> 3,180 / 3,136 us; profiles/r6c_*, r6d_*)
   int norm_once_mode() const {
-    static const int mode = getenv("TTS_NORM_ONCE") ? atoi(getenv("TTS_NORM_ONCE")) : 2;
+    static const int mode = getenv("TTS_NORM_ONCE") ? atoi(getenv("TTS_NORM_ONCE")) : 3;
     return mode;
   }
   bool norm_once_ok(int rows) const {
@@ -486,7 +489,7 @@ struct Ctx {
         a.norm_out = w.xn.as<bf16_t>() + (size_t)r0 * ldo;
       }
       const bool nrm = !p.sliced && epi == EPI_RESID && next_norm && norm_once_ok(rows) && decoding && rows == m &&
-                       (norm_once_mode() == 1 || nrm_region == 0);
+                       (norm_once_mode() == 1 || (norm_once_mode() == 2 && nrm_region == 0));
       if (nrm) set_norm_wgs(a, m, next_norm, w.xgran.as<uint64_t>() + xgran_region(nrm_region), N);
       launch_wgemm(a, p, epi, norm, s);
       if (fuse_norm || nrm) pending_norm = next_norm;
@@ -597,7 +600,7 @@ struct Ctx {
       if (fattn) {
         WgemmArgs fx = fused_attn_args(a, l, foproj);
         // (2..32 rows, o_proj fused: the ln2 RMSNorm once per row by appended workgroups)
-        const bool nrm = foproj && rows > 1 && norm_once_ok(rows);
+        const bool nrm = foproj && rows > 1 && norm_once_ok(rows) && norm_once_mode() <= 2;
         if (nrm) set_norm_wgs(fx, rows, ly.ln2, w.xgran.as<uint64_t>() + xgran_region(0), HID);
         gemm(w.x.as<bf16_t>(), rows, HID, ly.wqkv, QKV(), ly.ln1, w.qkv.as<bf16_t>(), QKV(), nullptr,
              EPI_STORE, &fx);
