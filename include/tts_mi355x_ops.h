@@ -33,7 +33,9 @@ tts_status tts_op_wgemm(const void* x, int32_t M, int32_t K, int32_t ldx, const 
                         void* resid, int32_t epi, void* stream);
 
 /* Prefill GEMM (many rows, one launch): same tiled weights and epilogues as tts_op_wgemm
- * (0 store, 1 residual, 2 SwiGLU), no fused RMSNorm, any M >= 1; N % 64 == 0, K % 64 == 0.
+ * (0 store, 1 residual, 2 SwiGLU), no fused RMSNorm, any M >= 1; N % 64 == 0, K % 128 == 0.
+ * Every output sums its K in the canonical 1024-element chunks, in order, so a row's bits do
+ * not depend on M or on the launch form (all of K per workgroup / one chunk per workgroup).
  * Replaces the per-token projections of transformers LlamaForCausalLM.forward over the
  * prompt (modeling_llama.py:163-176, 217-281) when the whole prompt batch is prefilled. */
 tts_status tts_op_pgemm(const void* x, int32_t M, int32_t K, const void* w_tiled, int32_t N, void* out,

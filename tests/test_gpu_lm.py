@@ -442,3 +442,24 @@ def test_decode_attention_long_context_vs_transformers(name, row_sets):
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         with open(os.path.join(ROOT, "gpurun_out", f"long_tf_dev_{name}.json"), "w") as f:
             json.dump({"bars": [bar_max, bar_mean], "by_rows": rec}, f, indent=1)
+
+
+def test_prefill_rows_do_not_depend_on_the_batch():
+    """The prefill GEMMs sum K in canonical 1024-chunks whatever their launch form (one chunk
+    per workgroup for a short prompt, the running sum in registers for a batch of prompts) and
+    the scored lm_head takes the decode GEMM's order at any row count, so a sequence scored or
+    generated alone gives the bits it gives inside a 20-sequence batch (202 rows alone: the
+    one-chunk form; 20 x ~200 rows: 128-row tiles)."""
+    from tts_amd import configs, synth
+
+    m = _model("tts1", 0x5EED, max_batch=20)
+    vocab = configs.vocab_for(configs.TTS1)
+    seqs = [synth.synthetic_prompt(vocab, u, 39, 150 + (u % 5)) for u in range(20)]
+    alone = m.score(seqs[:1], 4).numpy()
+    batch = m.score(seqs, 4).numpy()
+    assert np.array_equal(alone[0], batch[0])
+    one = m.generate_batch(seqs[:1], max_length=len(seqs[0]) + 6, min_new_tokens=6, eos_token_id=-1,
+                           repetition_penalty=1.1)[0]
+    many = m.generate_batch(seqs, max_length=max(len(s) for s in seqs) + 6, min_new_tokens=6, eos_token_id=-1,
+                            repetition_penalty=1.1)[0]
+    assert many[:len(one)] == one

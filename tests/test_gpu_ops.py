@@ -259,3 +259,32 @@ def test_pgemm_resid_swiglu(lib, M):
     scale = torch.maximum(h.float().abs(), y.abs())
     err = (res.cpu().float() - ref_res.float()).abs()
     assert (err > 4 * scale * 2.0 ** -8 + 1e-6).sum().item() == 0
+
+
+@pytest.mark.parametrize("epi,N,K", [(0, 3072, 2048), (1, 2048, 8192), (2, 2048, 2048), (0, 384, 256), (1, 4096, 14336)])
+def test_pgemm_rows_bit_identical_across_batch_sizes(lib, epi, N, K):
+    """Canonical K chunks: the first 65 rows of a prefill GEMM give the same bits whether the
+    launch holds 65, 202 (one canonical chunk per workgroup + the in-order combine), 300
+    (small tiles, the running sum in registers) or 700 rows (128-row tiles): a prompt's
+    prefill does not depend on the batch it is prefilled in."""
+    g = torch.Generator().manual_seed(epi * 7 + N + K)
+    x = (torch.randn(700, K, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.02).to(torch.bfloat16)
+    wt = _tiled(lib, w.cuda(), epi=epi)
+    nout = N // 2 if epi == 2 else N
+    base = (torch.randn(700, nout, generator=g) * 0.5).to(torch.bfloat16) if epi == 1 else None
+    got = {}
+    for M in (65, 202, 300, 700):
+        xd = x[:M].cuda()
+        if epi == 1:
+            res = base[:M].cuda()
+            _check(lib.tts_op_pgemm(xd.data_ptr(), M, K, wt.data_ptr(), N, None, nout, res.data_ptr(), 1, None))
+            torch.cuda.synchronize()
+            got[M] = res[:65].cpu()
+        else:
+            out = torch.empty(M, nout, dtype=torch.bfloat16, device="cuda")
+            _check(lib.tts_op_pgemm(xd.data_ptr(), M, K, wt.data_ptr(), N, out.data_ptr(), nout, None, epi, None))
+            torch.cuda.synchronize()
+            got[M] = out[:65].cpu()
+    for M in (202, 300, 700):
+        assert torch.equal(got[M], got[65]), (M, int((got[M] != got[65]).sum()))

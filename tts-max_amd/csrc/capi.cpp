@@ -392,8 +392,16 @@ tts_status tts_op_pgemm(const void* x, int32_t M, int32_t K, const void* w_tiled
     a.x = (const bf16_t*)x; a.M = M; a.K = K; a.ldx = K;
     a.w = (const bf16_t*)w_tiled; a.N = N;
     a.out = (bf16_t*)out; a.ldo = ldo; a.resid = (bf16_t*)resid;
-    launch_pgemm(a, epi, device_cu_count(), (hipStream_t)stream);
+    // the engine's scratch for the one-chunk-per-workgroup form (prompts of <= 256 rows,
+    // lm_engine.cpp kPgemmSplitRows): a stream-ordered allocation of this call's size
+    hipStream_t s = (hipStream_t)stream;
+    if (M <= 256) {
+      a.part_bytes = pgemm_part_bytes(M, N, K);
+      HIP_CHECK(hipMallocAsync((void**)&a.part, a.part_bytes, s));
+    }
+    launch_pgemm(a, epi, device_cu_count(), s);
     HIP_CHECK(hipGetLastError());
+    if (a.part) HIP_CHECK(hipFreeAsync(a.part, s));
   });
 }
 

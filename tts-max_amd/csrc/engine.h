@@ -90,6 +90,7 @@ struct LmWork {
   DevBuf epoch;                                     // decode-step counter (u32; the hand-off's tags)
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
+  DevBuf ppart;                                     // prefill GEMM fp32 partials [chunks][rows][N] (lm_pgemm.hip)
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]
   DevBuf counts;                                    // vLLM frequency penalty: new-token counts [B][V] u16
   DevBuf logits;                                    // scoring output (bf16)

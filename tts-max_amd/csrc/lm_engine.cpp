@@ -128,6 +128,16 @@ static size_t kpart_bytes(const tts_lm_config& c) {
   return (size_t)std::max(1, kmax / 2048) * kPrefillChunk * std::max(QKV, c.hidden_size) * 4;
 }
 
+// prefill GEMMs of <= kPgemmSplitRows rows may take one canonical K chunk per workgroup
+// (lm_pgemm.hip): fp32 partials [chunks][rows][N] of the largest of the layer's four GEMMs
+static constexpr int kPgemmSplitRows = 256;
+static size_t ppart_bytes(const tts_lm_config& c) {
+  const int H = c.hidden_size, HD = c.num_heads * c.head_dim, FF = c.intermediate_size;
+  const int QKV = (c.num_heads + 2 * c.num_kv_heads) * c.head_dim;
+  return std::max(std::max(pgemm_part_bytes(kPgemmSplitRows, QKV, H), pgemm_part_bytes(kPgemmSplitRows, H, HD)),
+                  std::max(pgemm_part_bytes(kPgemmSplitRows, 2 * FF, H), pgemm_part_bytes(kPgemmSplitRows, H, FF)));
+}
+
 void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int n) {
   TTS_REQUIRE(cfgp != nullptr, "null config");
   const tts_lm_config c = *cfgp;
@@ -259,6 +269,7 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   HIP_CHECK(hipMemsetAsync(w.epoch.p, 0, 64, s));
   HIP_CHECK(hipMemsetAsync(w.ferr.p, 0, 256, s));
   w.kpart.alloc(kpart_bytes(c));
+  w.ppart.alloc(ppart_bytes(c));
   w.slogits.alloc((size_t)B * V * 4);
   w.counts.alloc((size_t)B * (V / 32 + 1) * 32 * 2);
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
@@ -397,14 +408,20 @@ struct Ctx {
       // prefill: every prompt row of the batch in one LDS-staged MFMA launch
       const bf16_t* xin = x;
       if (normw) {
-        launch_rmsnorm(x, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, rows, K, s);
+        // (rows a residual combine already normalised with this weight: none to redo)
+        if (!(normw == ready && x == w.x.as<bf16_t>()))
+          launch_rmsnorm(x, K, normw, c.rms_norm_eps, w.xn.as<bf16_t>(), K, rows, K, s);
         xin = w.xn.as<bf16_t>();
       }
       PgemmArgs a;
       a.x = xin; a.M = rows; a.K = K; a.ldx = K;
       a.w = W; a.N = N;
       a.out = out; a.ldo = ldo; a.resid = resid;
-      launch_pgemm(a, epi, e->num_cu, s);
+      a.part = w.ppart.as<float>(); a.part_bytes = w.ppart.bytes;
+      if (resid == w.x.as<bf16_t>() && ldo == c.hidden_size && next_norm) {
+        a.next_norm = next_norm; a.eps = c.rms_norm_eps; a.xn = w.xn.as<bf16_t>();
+      }
+      if (launch_pgemm(a, epi, e->num_cu, s)) pending_norm = next_norm;
       return;
     }
     // decode GEMV launches hold at most 32 rows (two m-tiles: the A rows fit LDS); 33..64
@@ -627,13 +644,15 @@ struct Ctx {
       nrm_region = 0;
       if (!foproj)  // (decode: o_proj's combine may normalise with ln2 for the gate/up launch)
         gemm(w.attn_out.as<bf16_t>(), rows, HD, ly.wo, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID,
-             nullptr, decode ? ly.ln2 : nullptr);
+             nullptr, decode || rows > kPrefillChunk ? ly.ln2 : nullptr);
       gemm(w.x.as<bf16_t>(), rows, HID, ly.wgu, 2 * FF, ly.ln2, w.act.as<bf16_t>(), FF, nullptr,
            EPI_SWIGLU);
       const bf16_t* next_norm = (l + 1 < c.num_layers) ? M.layers[l + 1].ln1 : M.final_norm;
       nrm_region = 1;
-      gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(),
-           EPI_RESID, nullptr, decode ? next_norm : nullptr);
+      // (prefill GEMMs of > kPrefillChunk rows: the one-chunk form's combine may normalise too;
+      // not after the last layer, whose rows only the gathered lm_head rows read)
+      gemm(w.act.as<bf16_t>(), rows, FF, ly.wd, HID, nullptr, nullptr, HID, w.x.as<bf16_t>(), EPI_RESID, nullptr,
+           decode ? next_norm : (rows > kPrefillChunk && l + 1 < c.num_layers ? next_norm : nullptr));
     }
   }
 
@@ -1240,8 +1259,13 @@ void lm_score(Engine* e, const int32_t* ids, const int32_t* lens, int B, int n_l
   HIP_CHECK(hipMemcpyAsync(sel_d.p, sel.data(), nsel * 4, hipMemcpyHostToDevice, s));
   launch_gather_rows(e->w.x.as<bf16_t>(), c.hidden_size, sel_d.as<int>(), xs.as<bf16_t>(), nsel,
                      c.hidden_size, s);
-  X.gemm(xs.as<bf16_t>(), nsel, c.hidden_size, X.M.lm_head, c.vocab_size, X.M.final_norm,
-         lg.as<bf16_t>(), c.vocab_size, nullptr, EPI_STORE);
+  // the lm_head in launches of <= kPrefillChunk rows: the decode GEMM's K order, which the
+  // step's first token (B <= 64 gathered rows) also takes, so a sequence's logits do not depend
+  // on how many sequences are scored with it (the prefill GEMM sums K in 1024-chunks)
+  for (int r0 = 0; r0 < nsel; r0 += kPrefillChunk)
+    X.gemm(xs.as<bf16_t>() + (size_t)r0 * c.hidden_size, std::min(kPrefillChunk, nsel - r0), c.hidden_size,
+           X.M.lm_head, c.vocab_size, X.M.final_norm, lg.as<bf16_t>() + (size_t)r0 * c.vocab_size, c.vocab_size,
+           nullptr, EPI_STORE);
   check_launch();
   std::vector<uint16_t> h((size_t)nsel * c.vocab_size);
   HIP_CHECK(hipMemcpyAsync(h.data(), lg.p, h.size() * 2, hipMemcpyDeviceToHost, s));

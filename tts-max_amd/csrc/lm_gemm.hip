@@ -163,10 +163,13 @@ WgemmPlan plan_wgemm(int M, int N, int K, int epi, int num_cu) {
   // Residual projections with K chunks run K-sliced from 8 rows on even where the rows fit the
   // LDS prologue (TTS-1's down at 8..9 rows), so the per-row combine normalises each row once
   // for the next QKV launch (lm_engine.cpp, TTS_NORM_ONCE): 8 rows 753 -> 748 us a step; at 2 and 4
-  // rows it loses (671 -> 692, 706 -> 713 us; profiles/r6f_ab_slice_*.txt).  TTS_SLICE_RESID_ROWS=<n>
-  // moves the threshold (0: only where the rows do not fit)
+  // rows it loses (671 -> 692, 706 -> 713 us; profiles/r6f_ab_slice_*.txt).  Only matrices of
+  // four or more K chunks (a down projection): a 2-chunk o_proj (TTS-1-Max, K 4096) must keep the
+  // unsliced sum order of the o_proj that rides the 2..16-row QKV launch, so the separate and
+  // fused forms give the same bits.  TTS_SLICE_RESID_ROWS=<n> moves the threshold (0: only where
+  // the rows do not fit)
   static const int slice_rows = getenv("TTS_SLICE_RESID_ROWS") ? atoi(getenv("TTS_SLICE_RESID_ROWS")) : 8;
-  const bool force_slice = slice_rows > 0 && M >= slice_rows && epi == EPI_RESID;
+  const bool force_slice = slice_rows > 0 && M >= slice_rows && epi == EPI_RESID && p.sp.kc >= 4;
   if ((!p.a_lds || force_slice) && p.sp.kc > 1 && (epi == EPI_STORE || epi == EPI_RESID) &&
       wgemm_lds_bytes(w, ks, ng, M, K / p.sp.kc, true) <= kLdsBudget) {
     p.a_lds = true;

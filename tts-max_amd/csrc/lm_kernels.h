@@ -223,9 +223,18 @@ struct PgemmArgs {
   bf16_t* out = nullptr;  // [M][ldo]
   int ldo = 0;
   bf16_t* resid = nullptr;  // EPI_RESID: updated in place
+  int xcd_order = 0;        // set by launch_pgemm: the XCD-grouped tile order (lm_pgemm.hip)
+  float* part = nullptr;    // fp32 partials of the one-chunk-per-workgroup form (null: never used)
+  size_t part_bytes = 0;
+  // optional (EPI_RESID): the next RMSNorm of the updated rows, written to xn [M][N] by the
+  // one-chunk form's combine (launch_pgemm then returns true)
+  const bf16_t* next_norm = nullptr;
+  float eps = 0.f;
+  bf16_t* xn = nullptr;
 };
 bool pgemm_supported(int M, int N, int K, int epi);
-void launch_pgemm(const PgemmArgs& a, int epi, int num_cu, hipStream_t s);
+size_t pgemm_part_bytes(int M, int N, int K);  // the one-chunk form's partials of an M x N x K GEMM
+bool launch_pgemm(const PgemmArgs& a, int epi, int num_cu, hipStream_t s);  // true: xn written
 
 // ---- elementwise / small kernels (lm_ops.hip)
 void launch_rmsnorm(const bf16_t* x, int ldx, const bf16_t* w, float eps, bf16_t* y, int ldy,
