@@ -248,13 +248,11 @@ def sched_default_md5():
 
 
 @pytest.mark.parametrize("env", [{"TTS_CODEC_X3P": "0"}, {"TTS_CODEC_X3P_ILV": "0"}, {"TTS_CODEC_X3P_ILV": "1"},
-                                 {"TTS_CODEC_X3P_TILE": "5"}, {"TTS_CODEC_X3P_TILE": "4"}, {"TTS_CODEC_SPLIT": "0"},
-                                 {"TTS_CODEC_X3P_TILE": "4", "TTS_CODEC_X3P_SMALL4": "1"}],
-                         ids=["bx3", "ilv0", "ilv1", "tile5_3stage", "tile4_1wave", "nosplit", "tile4_4stage"])
+                                 {"TTS_CODEC_X3P_TILE": "5"}, {"TTS_CODEC_X3P_TILE": "4"},
+                                 {"TTS_CODEC_X3P_PP": "1"}, {"TTS_CODEC_X3P_TILE": "4", "TTS_CODEC_X3P_SMALL4": "1"}],
+                         ids=["bx3", "ilv0", "ilv1", "tile5_3stage", "tile4_1wave", "pp", "tile4_4stage"])
 def test_codec_gemm_schedules_same_bits(env, sched_default_md5):
     """Every codec GEMM form — the fp32-staging kernel, the planes kernel on each tile shape and
-    DMA schedule, one canonical K chunk per workgroup (the default at this batch's 2,600 rows)
-    or the chunks' running sum in registers — sums an output's K in the same order, so a
-    ragged batch decodes to the same bits under each (each form in its own process: the
-    switches are read once)."""
+    DMA schedule — sweeps an output's K in the same order, so a ragged batch decodes to the
+    same bits under each (each form in its own process: the switches are read once)."""
     assert _sched_md5(env) == sched_default_md5, env

@@ -63,6 +63,11 @@ CASES = [
     ("TTS_SLICED_GRID=0", "tts1", "24"),
     ("TTS_HEAD_GRID=512", "tts1", "1,24"),
     ("TTS_NORM_ONCE=0", "tts1", "8,16,24"),
+    # the prefill of the prefixes (score_decode prefills ~190 rows a sequence): one prompt takes
+    # the one-chunk-per-workgroup form, 8 prompts the running sum; both in the XCD tile order
+    ("TTS_PGEMM_XCD=0", "tts1", "1,8"),
+    ("TTS_PGEMM_SPLIT=0", "tts1", "1"),
+    ("TTS_PGEMM_SPLIT=1", "tts1", "1"),
     ("TTS_NORM_ONCE=0", "tts1-max-2l", "8"),
     ("TTS_BALANCE=0", "tts1-max-2l", "8"),
     ("TTS_FUSED_OPROJ_ROWS=0", "tts1-max-2l", "8"),

@@ -60,7 +60,6 @@ struct Codec {
   // same element offsets as the fp32 buffer they replace): b2 (RMSNorm / attention / GroupNorm +
   // swish outputs) and the fc1 -> fc2 hidden (4 D wide)
   DevBuf b2p, bigpp;
-  DevBuf part;  // gemm_x3p's split form: fp32 partials [chunks][rows][N] (passes of few rows)
   DevBuf rope_cs;  // [heads][32][cos, sin] of the attention's RoPE
   std::map<const float*, const uint16_t*> bplanes;
   DevBuf codes, wav;  // all utterances' codes; host-bound waveforms staged on the device
@@ -334,8 +333,6 @@ void gemm_p(const uint16_t* Ap, long long ap_plane, int M, int K, int lda, const
   g.Bp = it->second;
   g.C = C; g.ldc = ldc; g.resid = resid; g.act = act;
   g.Cp = Cp; g.cp_plane = cp_plane;
-  g.part = t_codec->part.bytes ? t_codec->part.as<float>() : nullptr;
-  g.part_elems = t_codec->part.bytes / 4;
   launch_gemm_x3p(g, s);
 }
 
@@ -456,12 +453,6 @@ static void decode_pass(Codec& cd, const int* codes_dev, const int32_t* lens, in
   if (xp) {
     grow(cd.b2p, (size_t)p2 * 3 * 2);
     grow(cd.bigpp, (size_t)pbig * 3 * 2);
-    // partials of the split form (a lone utterance's K > 1024 GEMMs: the embed conv, 7 chunks,
-    // the most); passes of more rows than kCodecSplitRows have tiles enough and never split
-    constexpr int kCodecSplitRows = 2048;
-    int cmax = D;
-    for (int i = 0; i < NU; ++i) cmax = std::max(cmax, cd.ups[i].Cout);
-    grow(cd.part, (size_t)8 * std::min(max_rows, kCodecSplitRows) * cmax * 4);
   }
   uint16_t* b2p = xp ? cd.b2p.as<uint16_t>() : nullptr;
   uint16_t* bigpp = xp ? cd.bigpp.as<uint16_t>() : nullptr;

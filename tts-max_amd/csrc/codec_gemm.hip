@@ -49,9 +49,7 @@ TTS_DEV u32x4_t lds_rd16(uint32_t addr) {
   return v;
 }
 
-// CH (K > kCodecKChunk): the canonical 1024-chunks summed in order by a running sum (a second
-// accumulator set); without it (K <= one chunk) the single chain is that sum already
-template <int TM, int TN, int WM, int WN, bool ILV, int NS = 2, bool CH = false>
+template <int TM, int TN, int WM, int WN, bool ILV, int NS = 2, bool PP = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int MI = TM / WM / 32, NJ = TN / WN / 32;  // 32x32 accumulators per wave
@@ -75,18 +73,17 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
   int tile = blockIdx.x;
   if (ntiles % 8 == 0) tile = (blockIdx.x % 8) * (ntiles / 8) + blockIdx.x / 8;
   const int m0 = (tile / nbn) * TM, n0 = (tile % nbn) * TN;
-  // K steps of 32: all of K (the running sum over the canonical 1024-chunks in registers), or
-  // one chunk = blockIdx.y (g.ksplit > 1: its fp32 partial to g.part, x3p_combine_kernel sums)
-  constexpr int CS = kCodecKChunk / 32;  // steps per chunk
-  const int s0 = g.ksplit > 1 ? (int)blockIdx.y * CS : 0;
-  const int nsteps = g.ksplit > 1 ? min(g.K / 32 - s0, CS) : g.K / 32;
+  const int nsteps = g.K / 32;
 
   // ---- per-lane DMA sources: row (lane >> 2) of each 16-row block, chunk (lane & 3) ^ swizzle
-  // (every wave issues QW pieces; round 5's out-of-phase split, half the waves issuing twice the
-  // pieces, measured slower: profiles/r5r_ab_codec_pp.txt)
-  constexpr int QD = QW, NL = NW;
-  const bool loader = true;
-  const int lw = wave;
+  // PP: only the upper half of the waves (one per SIMD) issue the DMA, twice the pieces each,
+  // between their first MFMA tiles; the lower half starts its MFMAs right after the barrier, so
+  // the two waves of a SIMD run out of phase and one of them is multiplying while the other
+  // issues or lands fragments
+  constexpr int QD = PP ? 2 * QW : QW;        // pieces per issuing wave
+  constexpr int NL = PP ? NW / 2 : NW;        // issuing waves
+  const bool loader = !PP || wave >= NW - NL;
+  const int lw = PP ? wave - (NW - NL) : wave;
   const int drow = lane >> 2;
   const int dchunk = (lane & 3) ^ ((lane >> 4) & 3);
   const uint16_t* srcp[QD];
@@ -97,12 +94,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
     if (q < QA) {
       const int p = q / (TM / 16), rb = q % (TM / 16);
       const int r = min(m0 + rb * 16 + drow, g.M - 1);
-      srcp[j] = g.Ap + p * g.ap_plane + (long long)r * g.lda + s0 * 32 + dchunk * 8;
+      srcp[j] = g.Ap + p * g.ap_plane + (long long)r * g.lda + dchunk * 8;
       dstoff[j] = p * APL + rb * 1024;
     } else {
       const int qb = q - QA, p = qb / (TN / 16), rb = qb % (TN / 16);
       const int r = min(n0 + rb * 16 + drow, g.N - 1);
-      srcp[j] = g.Bp + p * (long long)g.N * g.K + (long long)r * g.K + s0 * 32 + dchunk * 8;
+      srcp[j] = g.Bp + p * (long long)g.N * g.K + (long long)r * g.K + dchunk * 8;
       dstoff[j] = 3 * APL + p * BPL + rb * 1024;
     }
   }
@@ -135,31 +132,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
     }
   }
 
-  // acc: the current chunk's chain (from zero); tot: the finished chunks' sum, from +0, which
-  // adds exactly (a chain that starts at +0 never ends at -0), so for K <= 1024 tot is the
-  // chain itself and the split form's in-order combine gives the same bits
-  f32x16_t acc[MI][NJ], tot[MI][NJ];  // (tot: CH only)
+  f32x16_t acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[i][j][r] = 0.f;
-        if constexpr (CH) tot[i][j][r] = 0.f;
-      }
-  auto fold = [&]() {
-    if constexpr (CH) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          tot[i][j] += acc[i][j];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        }
-    }
-  };
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto bf = [](const u32x4_t& x) { return __builtin_bit_cast(bf16x8_t, x); };
   // the 3 (MI + NJ) fragments of k-slice kk of the stage at LDS byte address sb
@@ -261,7 +240,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
       const int nbuf = buf == 0 ? NS - 1 : buf - 1;
       compute(buf, s + NS - 1 < nsteps ? s + NS - 1 : -1, nbuf);
       buf = buf == NS - 1 ? 0 : buf + 1;
-      if (CH && (s + 1) % CS == 0) fold();
     }
   } else {
     // ---- two stages in flight; stage s is read after its DMA was counted in and every wave
@@ -275,25 +253,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
       compute(s & 1, -1, 0);
       asm volatile("s_barrier" ::: "memory");
       if (s + 2 < nsteps) issue(s + 2, s & 1);
-      if (CH && (s + 1) % CS == 0) fold();
     }
-  }
-  if (CH && nsteps % CS) fold();  // (the last, shorter chunk)
-  f32x16_t(&res)[MI][NJ] = *[&]() { if constexpr (CH) return &tot; else return &acc; }();
-
-  if (g.ksplit > 1) {  // one chunk: its fp32 partial (lane owns column lane & 31, as the fallback)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * (TN / WN) + j * 32 + (lane & 31);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * (TM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (m < g.M && n < g.N) g.part[((size_t)blockIdx.y * g.M + m) * g.N + n] = res[i][j][r];
-        }
-    }
-    return;
   }
 
   X3P_T(t_epi);
@@ -317,7 +277,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          tile[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * WTN + j * 32 + (lane & 31)] = res[i][j][r];
+          tile[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * WTN + j * 32 + (lane & 31)] = acc[i][j][r];
     constexpr int LPR = WTN / 4, RPI = 64 / LPR, IT = WTM / RPI;  // lanes per row, rows per instruction
     const int cq = lane % LPR, rr = lane / LPR;
     const int n = n0 + wn * WTN + 4 * cq;
@@ -386,7 +346,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = mb + (r & 3) + 8 * (r >> 2);
-          float v = res[i][j][r] + bias;
+          float v = acc[i][j][r] + bias;
           if (g.act == 1) v = v / (1.0f + expf(-v));
           if (has_resid) v = rv[r] + v;
           if (m < g.M && n < g.N) {
@@ -418,53 +378,23 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_x3p_kernel(GemmF32Args g) {
 #endif
 }
 
-// The split form's sum and epilogue: out(m, n) = epilogue(part[0] + part[1] + ...), the chunks
-// in order, with gemm_x3p_kernel's epilogue arithmetic (bias, swish, residual, fp32 and/or the
-// consumer's bf16 planes), one element per thread
-__global__ __launch_bounds__(256) void x3p_combine_kernel(GemmF32Args g, int nch) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)g.M * g.N) return;
-  const int m = (int)(i / g.N), n = (int)(i % g.N);
-  const size_t cs = (size_t)g.M * g.N;
-  float v = g.part[i];
-  for (int c = 1; c < nch; ++c) v += g.part[c * cs + i];
-  v = v + (g.bias ? g.bias[n] : 0.f);
-  if (g.act == 1) v = v / (1.0f + expf(-v));
-  const size_t o = (size_t)m * g.ldc + n;
-  if (g.resid) v = g.resid[o] + v;
-  if (g.C) g.C[o] = v;
-  if (g.Cp) {
-    asm("" : "+v"(v));  // (no contraction into v - h: see store_planes)
-    const float h = rbf(v), rm = v - h, mm = rbf(rm);
-    g.Cp[o] = f2bf(h);
-    g.Cp[g.cp_plane + o] = f2bf(mm);
-    g.Cp[2 * g.cp_plane + o] = f2bf(rm - mm);
-  }
-}
-
 template <int TM, int TN, int WM, int WN, int NS = 2>
 static void launch_x3p(const GemmF32Args& g, hipStream_t s) {
   constexpr size_t lds = NS * 3 * (size_t)(TM + TN) * 64;
   static_assert(lds <= 160 * 1024, "LDS");
   const int tiles = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
-  const dim3 grid(tiles, g.ksplit);  // (g.ksplit > 1: one canonical chunk per workgroup, then the combine)
   // the one-stage-ahead schedule with the DMA between the MFMAs on the 8- and 4-wave 64x64-per-
   // wave tiles (a step is long enough to cover the DMA's latency); the two-stage schedule on
   // the small tiles, whose steps are not (one 650-code utterance 4.8 -> 5.3 ms with the first,
   // profiles/r5h_ab_codec_ilv.txt).  TTS_CODEC_X3P_ILV=0 / 1 forces one (A/B)
   static const int ilv_env = getenv("TTS_CODEC_X3P_ILV") ? atoi(getenv("TTS_CODEC_X3P_ILV")) : -1;
   const bool ilv = NS >= 3 || (ilv_env >= 0 ? ilv_env != 0 : (TM / WM == 64 && TN / WN == 64));
-  // (PP, the out-of-phase DMA split on the 8-wave tile, measured slower in round 5 and is no
-  // longer launched: profiles/r5r_ab_codec_pp.txt)
-  const bool ch = g.K > kCodecKChunk;
-  if (ilv && ch) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS, true>), grid, dim3(64 * WM * WN), lds, s, g);
-  else if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS>), grid, dim3(64 * WM * WN), lds, s, g);
-  else if (ch) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false, 2, true>), grid, dim3(64 * WM * WN), lds, s, g);
-  else hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false>), grid, dim3(64 * WM * WN), lds, s, g);
-  if (g.ksplit > 1) {
-    const long long n = (long long)g.M * g.N;
-    hipLaunchKernelGGL(x3p_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, g.ksplit);
-  }
+  // TTS_CODEC_X3P_PP=1: the out-of-phase DMA split (PP, above) on the 8-wave tile (experiment)
+  static const bool pp = getenv("TTS_CODEC_X3P_PP") && atoi(getenv("TTS_CODEC_X3P_PP"));
+  if (ilv && pp && NS == 2 && WM * WN == 8)
+    hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS, WM * WN == 8>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  else if (ilv) hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, true, NS>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
+  else hipLaunchKernelGGL((gemm_x3p_kernel<TM, TN, WM, WN, false>), dim3(tiles), dim3(64 * WM * WN), lds, s, g);
 }
 
 static bool small4() {
@@ -477,9 +407,7 @@ bool gemm_x3p_supported(const GemmF32Args& g) {
   return g.Ap && g.Bp && g.K % 32 == 0 && g.lda % 8 == 0 && ((size_t)g.Ap & 15) == 0 && g.M >= 1 && g.N >= 1;
 }
 
-void launch_gemm_x3p(const GemmF32Args& g_in, hipStream_t s) {
-  GemmF32Args g = g_in;
-  g.ksplit = 1;
+void launch_gemm_x3p(const GemmF32Args& g, hipStream_t s) {
   if (!gemm_x3p_supported(g)) throw std::runtime_error("gemm_x3p: A and B planes, K % 32 == 0, 16-B aligned rows");
   // tiles: 256x128 (8 waves of 64x64, one workgroup per CU) where that makes >= 2 rounds of
   // the CUs (the ragged batch's big GEMMs); else 128x128, 128x64, 64x64 (4 waves) or 32x32 (one
@@ -492,27 +420,9 @@ void launch_gemm_x3p(const GemmF32Args& g_in, hipStream_t s) {
   int c = forced;
   if (c < 0)
     c = tiles(256, 128) >= 512 ? 0 : tiles(128, 128) >= 256 ? 1 : tiles(128, 64) >= 256 ? 2 : tiles(64, 64) >= 256 ? 3 : 4;
-  // few rows and K over one chunk (a lone utterance's fc2, resnet and embed convs): one chunk per
-  // workgroup on the largest tile whose tiles x chunks still fill the CUs (same bits).
-  // TTS_CODEC_SPLIT=0: off
-  static const bool split_on = !(getenv("TTS_CODEC_SPLIT") && !atoi(getenv("TTS_CODEC_SPLIT")));
-  const int nch = (g.K + kCodecKChunk - 1) / kCodecKChunk;
-  if (split_on && forced < 0 && c >= 2 && nch > 1 && g.part && (size_t)nch * g.M * g.N <= g.part_elems) {
-    g.ksplit = nch;
-    if (tiles(128, 128) * nch >= 256) launch_x3p<128, 128, 2, 4>(g, s);
-    else if (tiles(128, 64) * nch >= 256) launch_x3p<128, 64, 2, 2>(g, s);
-    else if (tiles(64, 64) * nch >= 256) launch_x3p<64, 64, 2, 2>(g, s);
-    else launch_x3p<32, 32, 1, 1>(g, s);
-    return;
-  }
   switch (c) {
     case 0: launch_x3p<256, 128, 4, 2>(g, s); break;
-    // (K over one chunk: 128 x 128 on 8 waves of 64 x 32 — on 4 waves of 64 x 64 the chunk
-    // running sum's second accumulator set leaves one wave per SIMD or spills)
-    case 1:
-      if (g.K > kCodecKChunk) launch_x3p<128, 128, 2, 4>(g, s);
-      else launch_x3p<128, 128, 2, 2>(g, s);
-      break;
+    case 1: launch_x3p<128, 128, 2, 2>(g, s); break;
     case 2: launch_x3p<128, 64, 2, 2>(g, s); break;
     case 3: launch_x3p<64, 64, 2, 2>(g, s); break;
     case 5: launch_x3p<128, 128, 2, 4, 3>(g, s); break;  // (8 waves of 64x32, three stages: experiment)

@@ -16,13 +16,6 @@ struct CodecSeg {
 
 // C[M][ldc] = act(A . B^T + bias) (+ resid), A row r at A + r*lda (lda may be < K: sliding
 // window view of a time-major activation = Conv1d without im2col), B [N][K] row-major.
-// Canonical K chunk of the codec's split-bf16 GEMMs (gemm_x3p, gemm_bx3): every output is the
-// in-order sum of its partial dot products over K = [0, 1024), [1024, 2048), ..., each one
-// MFMA chain from zero, whether one workgroup sweeps all of K (running sum in registers) or each
-// chunk runs on its own workgroup (split form: fp32 partials + an in-order combine).  So an
-// utterance's samples are the same decoded alone (few rows: the split form) or in a batch.
-constexpr int kCodecKChunk = 1024;
-
 struct GemmF32Args {
   const float* A = nullptr;
   int M = 0, K = 0, lda = 0;
@@ -43,8 +36,7 @@ struct GemmF32Args {
   uint16_t* Cp = nullptr;
   long long cp_plane = 0;
   // split-K over workgroups (fp32 partials [ksplit][M][N] in `part`, summed in split order by
-  // a reduce kernel): gemm_x3p's split form (one canonical chunk per workgroup) when `part`
-  // has room; the fp32 kernel's form is never used by launch_gemm_f32 (M-independent sums)
+  // a reduce kernel): kept by the kernels, never used by launch_gemm_f32 (M-independent sums)
   float* part = nullptr;
   size_t part_elems = 0;  // capacity of `part`
   int ksplit = 1, kchunk = 0;

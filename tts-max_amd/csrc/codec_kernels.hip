@@ -214,9 +214,7 @@ static void launch_split(GemmF32Args g, int target, hipStream_t s) {
 // Tile TM x TN over WM x WN waves, each wave (TM/WM) x (TN/WN) = MI x NJ accumulators of 32x32.
 // 64x64 and 128x128: 2 x 2 waves (256 threads); 256x128 / 256x256: 4 x 2 / 4 x 4 waves, each
 // 64x64 — half (a quarter) the operand bytes per MAC of the 128x128 tile, one workgroup per CU.
-// CH (K > kCodecKChunk): the canonical 1024-chunks, summed in order by a running sum (as
-// gemm_x3p_kernel, so both kernels keep giving the same bits)
-template <int TM, int TN, int WM, int WN, bool BPRE, bool APRE = false, bool CH = false>
+template <int TM, int TN, int WM, int WN, bool BPRE, bool APRE = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = 32, LS = BK + 8;           // bf16 row stride 80 B
@@ -244,29 +242,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
   const bf16_t* bq = BPRE ? (const bf16_t*)g.Bp + (size_t)(bok ? br : g.N - 1) * g.K + kbeg + bk : nullptr;
   const size_t bplane = (size_t)g.N * g.K;
   const u32x4_t zq = {0u, 0u, 0u, 0u};
-  f32x16_t acc[MI][NJ], tot[MI][NJ];  // (tot: CH only)
+  f32x16_t acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[i][j][r] = 0.f;
-        if constexpr (CH) tot[i][j][r] = 0.f;
-      }
-  auto fold = [&]() {
-    if constexpr (CH) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          tot[i][j] += acc[i][j];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        }
-    }
-  };
-  constexpr int CS = kCodecKChunk / BK;  // K steps per canonical chunk (chunk-aligned: kbeg = 0)
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   // two register sets: the global loads of step s+2 are in flight while step s computes
@@ -402,10 +384,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
     __syncthreads();
     load(st + 3, ra[1], rb[1], rq[1], raq[1]);
     if (st + 1 < nsteps) compute();
-    if (CH && (st + 2) % CS == 0) fold();
   }
-  if (CH && nsteps % CS) fold();
-  f32x16_t(&res)[MI][NJ] = *[&]() { if constexpr (CH) return &tot; else return &acc; }();
   // epilogue (as gemm_f32_kernel): lane owns column (lane & 31); rows (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -419,10 +398,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
         const int m = m0 + wm * (TM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= g.M) continue;
         if (g.ksplit > 1) {
-          g.part[((size_t)blockIdx.y * g.M + m) * g.N + n] = res[i][j][r];
+          g.part[((size_t)blockIdx.y * g.M + m) * g.N + n] = acc[i][j][r];
           continue;
         }
-        float v = res[i][j][r] + bias;
+        float v = acc[i][j][r] + bias;
         if (g.act == 1) v = v / (1.0f + expf(-v));
         if (g.resid) v = g.resid[(size_t)m * g.ldc + n] + v;
         if (g.C) g.C[(size_t)m * g.ldc + n] = v;
@@ -431,25 +410,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bx3_kernel(GemmF32Args g) {
   }
 }
 
-// gemm_bx3_kernel with the chunk running sum where K spans more than one canonical chunk
-// (the 8-wave 256 x 128 tile has no registers for the running sum: K <= one chunk only)
-template <int TM, int TN, int WM, int WN, bool BPRE, bool APRE = false>
-static void launch_bx3(const GemmF32Args& g, dim3 grid, hipStream_t s) {
-  constexpr bool ch_ok = !(TM == 256 && TN == 128);
-  if (g.K > kCodecKChunk) {
-    if constexpr (ch_ok)
-      hipLaunchKernelGGL((gemm_bx3_kernel<TM, TN, WM, WN, BPRE, APRE, true>), grid, dim3(64 * WM * WN), 0, s, g);
-    else
-      throw std::runtime_error("gemm_bx3: the 256 x 128 tile takes K <= one chunk");
-  } else {
-    hipLaunchKernelGGL((gemm_bx3_kernel<TM, TN, WM, WN, BPRE, APRE, false>), grid, dim3(64 * WM * WN), 0, s, g);
-  }
-}
-
-// Every output element sums K in the canonical chunks, in order, whatever the tile shape, so a
-// row's bits do not depend on how many rows share the launch (an utterance decodes to the same
-// samples alone or in any batch).  This launcher never splits K over workgroups (gemm_x3p's
-// launcher does, for few rows: same bits).
+// The codec never splits K over workgroups: every output element is one in-order sweep of K
+// whatever the tile shape, so a row's bits do not depend on how many rows share the launch
+// (an utterance decodes to the same samples alone or in any batch).  A ragged batch gives
+// the GEMMs their rows; a lone short utterance leaves CUs idle instead.
 void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
   GemmF32Args g = g_in;
   g.part = nullptr;
@@ -465,21 +429,20 @@ void launch_gemm_f32(const GemmF32Args& g_in, hipStream_t s) {
     // split for twice the outputs) where those tiles still make >= 2 rounds of the CUs (the
     // ragged batch's big GEMMs).  (256x256 on 16 waves spills: 4 waves per SIMD leave 128 VGPRs)
     static const int big_tiles = getenv("TTS_CODEC_TILE") ? atoi(getenv("TTS_CODEC_TILE")) : 1;
-    // (K over one canonical chunk: not on 256 x 128, launch_bx3)
-    const int t21 = g.K > kCodecKChunk ? 0 : ((g.M + 255) / 256) * ((g.N + 127) / 128);
+    const int t21 = ((g.M + 255) / 256) * ((g.N + 127) / 128);
     const int t12 = ((g.M + 127) / 128) * ((g.N + 255) / 256);
     if (g.Bp && g.Ap && big_tiles == 1 && t21 >= 2 * 256)
-      launch_bx3<256, 128, 4, 2, true, true>(g, dim3(t21), s);
+      hipLaunchKernelGGL((gemm_bx3_kernel<256, 128, 4, 2, true, true>), dim3(t21), dim3(512), 0, s, g);
     else if (g.Bp && g.Ap && big >= 256)
-      launch_bx3<128, 128, 2, 2, true, true>(g, g128, s);
+      hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, 2, 2, true, true>), g128, dim3(256), 0, s, g);
     else if (g.Bp && big_tiles == 1 && t21 >= 2 * 256)
-      launch_bx3<256, 128, 4, 2, true>(g, dim3(t21), s);
+      hipLaunchKernelGGL((gemm_bx3_kernel<256, 128, 4, 2, true>), dim3(t21), dim3(512), 0, s, g);
     else if (g.Bp && big_tiles == 2 && t12 >= 2 * 256)
-      launch_bx3<128, 256, 2, 4, true>(g, dim3(t12), s);
-    else if (g.Bp && big >= 256) launch_bx3<128, 128, 2, 2, true>(g, g128, s);
-    else if (g.Bp) launch_bx3<64, 64, 2, 2, true>(g, g64, s);
-    else if (big >= 256) launch_bx3<128, 128, 2, 2, false>(g, g128, s);
-    else launch_bx3<64, 64, 2, 2, false>(g, g64, s);
+      hipLaunchKernelGGL((gemm_bx3_kernel<128, 256, 2, 4, true>), dim3(t12), dim3(512), 0, s, g);
+    else if (g.Bp && big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, 2, 2, true>), g128, dim3(256), 0, s, g);
+    else if (g.Bp) hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, 2, 2, true>), g64, dim3(256), 0, s, g);
+    else if (big >= 256) hipLaunchKernelGGL((gemm_bx3_kernel<128, 128, 2, 2, false>), g128, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_bx3_kernel<64, 64, 2, 2, false>), g64, dim3(256), 0, s, g);
     return;
   }
   if (big >= 256) launch_split<128, 128>(g, 0, s);
