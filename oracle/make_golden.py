@@ -148,6 +148,10 @@ CHAIN_CASES = {
         (2, 60, dict(new=120, min_new=120, rep=1.0), "single"),
         (3, 700, dict(new=200, min_new=200, rep=1.4), "single"),
     ] + [(10 + r, 10 + 190 * r, dict(new=200, min_new=200, rep=1.1), "batch") for r in range(8)]),
+    # configs[3]'s length at full depth: 500 codes, EOS masked (the bench shape, rep 1.1)
+    "lm_chain_max500": ("tts1-max", 0x5EED, [
+        (0, 300, dict(new=500, min_new=500, rep=1.1), "single"),
+    ]),
 }
 
 

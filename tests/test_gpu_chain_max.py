@@ -8,6 +8,8 @@ oracle/make_golden.py --only lm_chain_max.  Each step is decided by a margin far
 implementation noise (the manifest's hf_min_margin against top2_dev_vs_oracle_max), so a
 single differing id fails.  Runs the HF-form surface at batch 1 and the graph-captured
 batched decode at 8 rows (configs[3]'s per-GPU shard: 64 prompts over 8 GPUs) and 24 rows.
+tests/golden/lm_chain_max500.npz (oracle/make_golden.py --only lm_chain_max500) holds one
+500-id sequence, configs[3]'s length (prompt 170 + 500 codes, EOS masked, penalty 1.1).
 """
 
 import json
@@ -21,10 +23,11 @@ pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FIXTURE = os.path.join(GOLDEN, "lm_chain_max.npz")
+FIXTURE500 = os.path.join(GOLDEN, "lm_chain_max500.npz")
 
 
-def _cases():
-    z = np.load(FIXTURE)
+def _cases(path=FIXTURE):
+    z = np.load(path)
     out, po, no = [], 0, 0
     for i, P in enumerate(z["prompt_lens"]):
         n = int(z["hf_new_lens"][i])
@@ -46,7 +49,7 @@ def _lm():
     if "m" not in _model:
         arch_name, seed, spec, _ = _cases()
         _model["m"] = MI355XSpeechLM.synthetic(configs.LM_ARCHS[arch_name], seed=seed, chain=synth.ChainSpec(**spec),
-                                               max_batch=24, max_seq_len=640)
+                                               max_batch=24, max_seq_len=720)
     return _model["m"]
 
 
@@ -85,3 +88,24 @@ def test_max_chain_batched_rows(rows):
     for r, o in enumerate(outs):
         ref = grp[r % 8]["hf_new"]
         assert o[:new_n] == ref, (r, next(i for i, (a, b) in enumerate(zip(o, ref)) if a != b))
+
+
+def test_max_chain_500_codes():
+    """configs[3]'s length at full depth: transformers' 500 ids for the bench-shaped case, id
+    for id, through the HF-form surface and as 8 copies in the graph-captured decode (the
+    per-GPU shard's row count)."""
+    arch, seed, spec, cases = _cases(FIXTURE500)
+    assert (arch, seed, spec) == _cases()[:3]  # (the model of the other chain tests)
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))["lm_chain_max500"]
+    c, mc = cases[0], man["cases"][0]
+    assert len(c["hf_new"]) == 500 and mc["hf_min_margin"] >= 4 * max(mc["top2_dev_vs_oracle_max"], 1.0), mc
+    m = _lm()
+    out = m.generate(input_ids=torch.tensor([c["prompt"]]), max_length=c["max_length"],
+                     min_new_tokens=c["min_new"], eos_token_id=c["eos"], do_sample=False,
+                     repetition_penalty=c["rep"], top_p=1.0, temperature=0.0)
+    new = out[0, len(c["prompt"]):].tolist()
+    assert new == c["hf_new"], next(i for i, (a, b) in enumerate(zip(new + [-9], c["hf_new"] + [-8])) if a != b)
+    outs = m.generate_batch([c["prompt"]] * 8, max_length=c["max_length"], min_new_tokens=c["min_new"],
+                            eos_token_id=c["eos"], repetition_penalty=c["rep"])
+    for r, o in enumerate(outs):
+        assert o[:500] == c["hf_new"], (r, next(i for i, (a, b) in enumerate(zip(o, c["hf_new"])) if a != b))
