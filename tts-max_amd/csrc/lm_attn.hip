@@ -14,6 +14,8 @@
 // the A-operand layouts of S^T = K.Q^T and O^T = V^T.P^T on v_mfma_f32_16x16x32_bf16, so the
 // kernels load every fragment straight into registers.  Both kernels write the attention
 // output (bf16, [rows][H*D]) directly: no chunk partials, no merge pass.
+#include <stdexcept>
+
 #include "hip_common.h"
 #include "lm_kernels.h"
 #include "lm_attn_core.h"
@@ -26,26 +28,46 @@ TTS_DEV float rope_at(const bf16_t* v, int d, const bf16_t* cosr, const bf16_t* 
   return rope_elem(v[d], v[d < H2 ? d + H2 : d - H2], d < H2, bf2f(cosr[d]), bf2f(sinr[d]));
 }
 
-// Prefill: rope q -> q_rot, rope k -> K rows, v -> V^T columns, for every row.
+// Prefill: rope q -> q_rot, rope k -> K rows, v -> V^T columns.  Workgroups [0, rows): the
+// rope of one row's q and k.  Workgroups [rows, rows + nblocks): the V^T columns of one query
+// block (up to 16 consecutive positions of one sequence, a.blocks) — a row's V lands in a
+// different 64-B row of every V^T tile, so writing it row by row stored 2 B per 64-B segment
+// (a 32-prompt prefill's appends took 38 us a layer, most of it this write amplification);
+// the block's V rows are staged in LDS and written with consecutive lanes on consecutive
+// positions (16 positions = 32 contiguous bytes of a V^T tile row).
 template <int D>
-__global__ void rope_append_kernel(AttnArgs a) {
-  const int row = blockIdx.x;
-  const int slot = a.row_slot[row], pos = a.row_pos[row];
-  const bf16_t* base = a.qkv + (size_t)row * a.ld_qkv;
-  const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
-  const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
+__global__ __launch_bounds__(256) void rope_append_kernel(AttnArgs a) {
+  constexpr int VLD = 8 * D + 8;  // staged V row stride (bf16, KVH <= 8): +16 B spreads the rows' banks
+  __shared__ __attribute__((aligned(16))) bf16_t vs[16 * VLD];
   const int HD = a.H * D, KD = a.KVH * D;
-  for (int i = threadIdx.x; i < HD + 2 * KD; i += blockDim.x) {
-    if (i < HD) {
-      const int h = i / D, d = i % D;
-      a.q_rot[(size_t)row * HD + i] = f2bf(rope_at<D>(base + h * D, d, cosr, sinr));
-    } else if (i < HD + KD) {
-      const int j = i - HD, h = j / D, d = j % D;
-      a.kcache[(((size_t)slot * a.KVH + h) * a.max_seq + pos) * D + d] = f2bf(rope_at<D>(base + HD + h * D, d, cosr, sinr));
-    } else {
-      const int j = i - HD - KD, h = j / D, d = j % D;
-      a.vtcache[((size_t)slot * a.KVH + h) * D * a.max_seq + vt_off(a.max_seq, d, pos)] = base[HD + KD + j];
+  if ((int)blockIdx.x < a.rows) {
+    const int row = blockIdx.x;
+    const int slot = a.row_slot[row], pos = a.row_pos[row];
+    const bf16_t* base = a.qkv + (size_t)row * a.ld_qkv;
+    const bf16_t* cosr = a.rope_cos + (size_t)pos * D;
+    const bf16_t* sinr = a.rope_sin + (size_t)pos * D;
+    for (int i = threadIdx.x; i < HD + KD; i += blockDim.x) {
+      if (i < HD) {
+        const int h = i / D, d = i % D;
+        a.q_rot[(size_t)row * HD + i] = f2bf(rope_at<D>(base + h * D, d, cosr, sinr));
+      } else {
+        const int j = i - HD, h = j / D, d = j % D;
+        a.kcache[(((size_t)slot * a.KVH + h) * a.max_seq + pos) * D + d] = f2bf(rope_at<D>(base + HD + h * D, d, cosr, sinr));
+      }
     }
+    return;
+  }
+  const int4 blk = a.blocks[blockIdx.x - a.rows];  // {first row, rows, slot, first position}
+  const int r0 = blk.x, nr = blk.y, slot = blk.z, p0 = blk.w;
+  for (int e = threadIdx.x; e < nr * (KD / 8); e += blockDim.x) {  // the block's V rows, 16 B a thread
+    const int rr = e / (KD / 8), c = e - rr * (KD / 8);
+    *(u32x4_t*)(vs + rr * VLD + c * 8) = *(const u32x4_t*)(a.qkv + (size_t)(r0 + rr) * a.ld_qkv + HD + KD + c * 8);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < KD * 16; e += blockDim.x) {
+    const int j = e >> 4, pl = e & 15, h = j / D, d = j % D;
+    if (pl < nr)
+      a.vtcache[((size_t)slot * a.KVH + h) * D * a.max_seq + vt_off(a.max_seq, d, p0 + pl)] = vs[pl * VLD + j];
   }
 }
 
@@ -222,8 +244,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnArgs a) {
 }
 
 void launch_rope_append(const AttnArgs& a, hipStream_t s) {
-  if (a.D == 64) hipLaunchKernelGGL(rope_append_kernel<64>, dim3(a.rows), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(rope_append_kernel<128>, dim3(a.rows), dim3(256), 0, s, a);
+  if (a.KVH > 8) throw std::runtime_error("rope_append: at most 8 kv heads");
+  if (a.D == 64) hipLaunchKernelGGL(rope_append_kernel<64>, dim3(a.rows + a.nblocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(rope_append_kernel<128>, dim3(a.rows + a.nblocks), dim3(256), 0, s, a);
 }
 
 void launch_attn_prefill(const AttnArgs& a, hipStream_t s) {
