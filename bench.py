@@ -229,14 +229,28 @@ def main():
         fused_o = True
     except Exception:  # noqa: BLE001 (not this shape: separate launches)
         pass
-    # per-step share: the layer kernels once per layer, lm_head once
+    # the greedy step's lm_head: the int8 screen + exact recheck of the tiles that can hold the
+    # argmax (lm_head_screen.hip; TTS_HEAD_SCREEN=0: the full bf16 lm_head launch)
+    screened = False
+    if os.environ.get("TTS_HEAD_SCREEN", "1") != "0":
+        try:
+            for k in ("head_screened", "head_screen"):
+                ms, by = lm.bench_kernel(k, rows=B, ctx=ctx_mid, iters=args.kernel_iters)
+                kern[k] = dict(avg_ms=ms, bytes=by, gbs=by / ms / 1e6)
+            screened = True
+        except Exception:  # noqa: BLE001 (not this shape: the full lm_head)
+            pass
+    # per-step share: the layer kernels once per layer, the head once
     in_step = [k for k in kern if not (fused and k in ("qkv", "attention"))
-               and not (fused_o and k in ("qkv_attn", "o_proj"))]
-    share = {k: kern[k]["avg_ms"] * (1 if k == "lm_head" else arch.num_layers) for k in in_step}
+               and not (fused_o and k in ("qkv_attn", "o_proj")) and k != "head_screen"
+               and not (screened and k == "lm_head")]
+    share = {k: kern[k]["avg_ms"] * (1 if k in ("lm_head", "head_screened") else arch.num_layers) for k in in_step}
     dom = max(share, key=share.get)
     step_ms = lm_decode / max(dec_steps, 1)
     kv_ctx_bytes = B * arch.kv_bytes_per_token() * ctx_mid
     step_bytes = arch.weight_bytes_per_step() + kv_ctx_bytes
+    if screened:  # (the int8 head and its recheck instead of the bf16 lm_head's V x hidden x 2 bytes)
+        step_bytes += round(kern["head_screened"]["bytes"]) - 2 * arch.vocab_size * arch.hidden_size
     # HBM traffic of that kernel from the PMC passes of scripts/pmc_traffic.sh (FETCH_SIZE x2
     # + WRITE_SIZE per launch, committed under profiles/), when one exists for this shape
     def pmc(k, rows):
@@ -295,7 +309,7 @@ def main():
                            prefill_roofline=prefill_roofline(arch, [len(q) for q in p32], a32))
         # the 32-row decode kernels: live HIP-event time, algorithmic bytes, PMC HBM traffic
         k32s = {}
-        for k in lm.KERNELS:
+        for k in lm.KERNELS:  # (32 rows: the full lm_head; the screen takes <= 16)
             ms, by = lm.bench_kernel(k, rows=32, ctx=ctx_mid, iters=args.kernel_iters)
             k32s[k] = dict(avg_ms=round(ms, 5), bytes=round(by), gbs=round(by / ms / 1e6, 1), traffic=pmc(k, 32)[0])
         sec["bs32"]["kernels"] = k32s

@@ -201,7 +201,9 @@ tts_status tts_lm_last_timing(tts_engine* e, float* prefill_ms, float* decode_ms
  * (+RMSNorm, SwiGLU), 3 down_proj (+residual), 4 lm_head (+RMSNorm, penalty, argmax
  * partials), 5 decode attention (ctx = `ctx` positions), 6 qkv with the decode attention
  * fused in (1..16 rows where that form applies), 7 the same launch also carrying o_proj
- * (+residual; the 1..16-row step's default form where the shapes allow).  rows = batch rows.
+ * (+residual; the 1..16-row step's default form where the shapes allow), 8 the greedy step's
+ * screened lm_head (int8 screen + exact recheck of the tiles that can hold the argmax; <= 32
+ * rows), 9 its int8 screen alone.  rows = batch rows.
  * Outputs: average ms per launch and the algorithmic HBM bytes one launch must move. */
 tts_status tts_lm_bench_kernel(tts_engine* e, int32_t which, int32_t rows, int32_t ctx,
                                int32_t iters, float* avg_ms, double* bytes);

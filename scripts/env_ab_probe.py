@@ -17,7 +17,7 @@ rows = int(sys.argv[2])
 arch = configs.LM_ARCHS[os.environ.get("AB_ARCH", "tts1")]
 m = MI355XSpeechLM.synthetic(arch, max_batch=max(rows, 1), max_seq_len=720)
 r = {}
-for k in list(m.KERNELS) + ["qkv_attn", "qkv_attn_oproj"]:  # (the fused forms where they apply)
+for k in list(m.KERNELS) + ["qkv_attn", "qkv_attn_oproj", "head_screened", "head_screen"]:  # (the fused forms where they apply)
     try:
         r[k] = round(m.bench_kernel(k, rows=rows, ctx=450, iters=64)[0] * 1000, 2)
     except Exception:

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 6: the greedy lm_head as an int8 screen + exact recheck (lm_head_screen.hip): its parity
+# tests (screened ids == the full lm_head's, the bound check, exact ties), the same-bits switch,
+# a same-box A/B of TTS_HEAD_SCREEN at 1 / 8 / 32 rows, the bench line
+set -u
+O=gpurun_out
+T=${1:-r6s}
+mkdir -p $O
+export TMPDIR=/tmp
+fatal() { if [ $1 -ne 0 ]; then echo "stop: rc=$1 in $2"; exit $1; fi; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_head_screen.py tests/test_gpu_switches.py -k "head or HEAD" -v -rf --timeout 400 --timeout-method thread > $O/${T}_tests.log 2>&1; rc=$?
+tail -12 $O/${T}_tests.log; fatal $rc tests
+for r in 1 8 16; do
+  timeout -k 10 600 python -u scripts/env_ab_probe.py TTS_HEAD_SCREEN $r 2 > $O/${T}_ab_head_screen_$r.txt 2>&1; rc=$?
+  cat $O/${T}_ab_head_screen_$r.txt; fatal $rc ab$r
+done
+AB_ARCH=tts1-max timeout -k 10 600 python -u scripts/env_ab_probe.py TTS_HEAD_SCREEN 8 2 > $O/${T}_ab_head_screen_max8.txt 2>&1; rc=$?
+cat $O/${T}_ab_head_screen_max8.txt; fatal $rc abmax8
+timeout -k 10 600 python bench.py > $O/${T}_bench.json 2> $O/${T}_bench.err; rc=$?
+tail -3 $O/${T}_bench.err; cat $O/${T}_bench.json; fatal $rc bench
+echo done

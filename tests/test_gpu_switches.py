@@ -71,6 +71,11 @@ CASES = [
     ("TTS_NORM_ONCE=0", "tts1-max-2l", "8"),
     ("TTS_BALANCE=0", "tts1-max-2l", "8"),
     ("TTS_FUSED_OPROJ_ROWS=0", "tts1-max-2l", "8"),
+    # the greedy lm_head's int8 screen + exact recheck: the full lm_head's ids
+    ("TTS_HEAD_SCREEN=0", "tts1", "1,8,24"),
+    ("TTS_HEAD_SCREEN=0", "tts1-max-2l", "8"),
+    ("TTS_HEAD_SCREEN_WAIT=0", "tts1", "1,8"),
+    ("TTS_HEAD_SCREEN_WAIT=1", "tts1", "1,8"),
 ]
 
 

@@ -45,7 +45,7 @@ def _hot_wgemm():
 
 
 UNITS = ["lm_gemm_store.hip", "lm_gemm_resid.hip", "lm_gemm_swiglu.hip", "lm_gemm_logits.hip", "lm_attn.hip",
-         "lm_ops.hip", "lm_pgemm.hip", "codec_kernels.hip", "codec_gemm.hip"]
+         "lm_ops.hip", "lm_pgemm.hip", "codec_kernels.hip", "codec_gemm.hip", "lm_head_screen.hip"]
 
 pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 
@@ -88,7 +88,8 @@ def spills():
 
 def test_step_plan_lists_the_bench_launches():
     """The dry run reproduces the launch structure the GPU runs: the one-row step is three
-    launches a layer + lm_head + finalize (QKV + attention + o_proj fused, gate/up, down)."""
+    launches a layer (QKV + attention + o_proj fused, gate/up, down) + the greedy head (int8
+    screen + exact recompute of the units that can hold the argmax, lm_head_screen.hip) + finalize."""
     import sys
 
     sys.path.insert(0, os.path.join(ROOT, "tts-max_amd"))
@@ -96,8 +97,8 @@ def test_step_plan_lists_the_bench_launches():
     from tts_amd.speechlm import step_plan
 
     one = step_plan(configs.LM_ARCHS["tts1"], 1)
-    assert one[-1] == "finalize_greedy_kernel"
-    assert len([k for k in one if k.startswith("wgemm_kernel<")]) == 4, one
+    assert one[-2:] == ["head_screen_kernel<1, 32, 1>", "finalize_greedy_kernel"], one
+    assert len([k for k in one if k.startswith("wgemm_kernel<")]) == 3, one
     assert "attn_decode_kernel<64>" not in one  # (fused into the QKV launch)
     b32 = step_plan(configs.LM_ARCHS["tts1"], 32)
     assert "attn_decode_kernel<64>" in b32 and "splitk_combine_norm" in b32, b32
@@ -124,5 +125,6 @@ def test_hot_wgemm_instantiations_do_not_spill(spills):
 
 def test_attention_finalize_prefill_codec_kernels_do_not_spill(spills):
     bad = {k: n for k, (unit, n) in spills.items()
-           if unit in ("lm_attn.hip", "lm_ops.hip", "lm_pgemm.hip", "codec_kernels.hip", "codec_gemm.hip") and n > 0}
+           if unit in ("lm_attn.hip", "lm_ops.hip", "lm_pgemm.hip", "codec_kernels.hip", "codec_gemm.hip",
+                       "lm_head_screen.hip") and n > 0}
     assert not bad, f"VGPR spills: {bad}"

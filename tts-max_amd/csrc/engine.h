@@ -72,6 +72,10 @@ struct LmModel {
   std::vector<LmLayer> layers;
   bf16_t* final_norm = nullptr;
   bf16_t* lm_head = nullptr;  // tiled [V][hidden]
+  // the greedy lm_head's int8 screen (lm_head_screen.hip): codes in the screen's block layout,
+  // per-column {scale, |W - Wh|, |W|, |Wh|}; head_grid = the screen's launch grid (0: none)
+  DevBuf head_q, head_c;
+  int head_grid = 0;
   std::vector<int> id_to_code;  // host LUT (optional)
   int qkv_n() const { return (cfg.num_heads + 2 * cfg.num_kv_heads) * cfg.head_dim; }
 };
@@ -89,6 +93,7 @@ struct LmWork {
   DevBuf xgran;                                     // norm-once hand-off: hidden-row granules [2][B][hidden/2] u64
   DevBuf epoch;                                     // decode-step counter (u32; the hand-off's tags)
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
+  DevBuf hub, hlb;                                  // screened head: check-mode score bounds [B][V], per-row max lower bound (u64)
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf ppart;                                     // prefill GEMM fp32 partials [chunks][rows][N] (lm_pgemm.hip)
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]

@@ -24,6 +24,12 @@ static constexpr int kPollEvery = 8;
 static constexpr int kPrefillChunk = 64;   // rows per GEMM launch (MFMA A-tiles of 16)
 static constexpr int kMaxPrefillRows = 8192;
 
+// the greedy lm_head's int8 screen + exact recheck (lm_head_screen.hip); TTS_HEAD_SCREEN=0: off
+static bool head_screen_enabled() {
+  static const bool v = !(getenv("TTS_HEAD_SCREEN") && !atoi(getenv("TTS_HEAD_SCREEN")));
+  return v;
+}
+
 int64_t numel(const tts_tensor_desc& d) {
   int64_t n = 1;
   for (int i = 0; i < d.ndim; ++i) n *= d.shape[i];
@@ -216,6 +222,22 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   } else {
     retiled(tm.get("lm_head.weight", {V, HID}), M.lm_head, V, HID, V, 1, 1, 0);
   }
+  // the greedy lm_head's int8 screen (lm_head_screen.hip; TTS_HEAD_SCREEN=0: none), made from
+  // the row-major matrix (the embedding rows when tied, else the staged upload)
+  M.head_grid = 0;
+  M.head_q.release();
+  M.head_c.release();
+  {
+    const StreamPlan hp = stream_plan(V, HID, 1, ncu);
+    if (head_screen_enabled() && head_screen_supported(1, HID, V) && hp.ng == 1 && hp.ksplit == 1) {
+      M.head_grid = ncu;
+      M.head_q.alloc((size_t)V * HID);
+      M.head_c.alloc((size_t)V * 16);
+      launch_head_quant(c.tie_word_embeddings ? M.embed_rows.as<bf16_t>() : staging.as<bf16_t>(), V, HID,
+                        M.head_grid * head_screen_waves(), M.head_q.as<int8_t>(), M.head_c.as<float>(), s);
+      HIP_CHECK(hipGetLastError());
+    }
+  }
 
   // ---- RoPE table
   M.rope.alloc((size_t)2 * c.max_seq_len * D * 2);
@@ -274,6 +296,13 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.counts.alloc((size_t)B * (V / 32 + 1) * 32 * 2);
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
+  if (M.head_grid) {
+    w.hub.alloc((size_t)std::min(B, 16) * V * 4);
+    w.hlb.alloc(16 * 8 * 8 + 8 * 64);  // 16 rows x 8 shards of bounds + 8 arrival counters (64 B apart)
+    HIP_CHECK(hipMemsetAsync(w.hlb.p, 0, w.hlb.bytes, s));  // (below any step's key)
+  } else {
+    w.hub.release(); w.hlb.release();
+  }
   w.row_slot.alloc((size_t)R * 4);
   w.row_pos.alloc((size_t)R * 4);
   w.row_idx.alloc((size_t)R * 4);
@@ -345,6 +374,22 @@ bool use_fused_oproj_rows() {
 // canonical sum order: the same bits)
 bool norm_prologue32() {
   static const bool v = getenv("TTS_NORM_PROLOGUE32") && atoi(getenv("TTS_NORM_PROLOGUE32"));
+  return v;
+}
+
+// The greedy lm_head as an exact two-pass argmax (lm_head_screen.hip): default on;
+// TTS_HEAD_SCREEN=0 streams the full bf16 lm_head for greedy steps too (the same ids);
+// TTS_HEAD_SCREEN_CHECK=1 recomputes every tile and checks each score against its bound
+// ... whose workgroups wait for every workgroup's bounds before flagging their units (the
+// exact candidate set; TTS_HEAD_SCREEN_WAIT=0: never, 1: always, n > 1 (default 2): from n rows —
+// one row: 69 vs 73 us, 8 rows: 79 vs 96 us without, profiles/r6w_ab_head_wait_*).  Same bits
+// either way: a lower LB only flags more units
+bool head_screen_wait(int rows) {
+  static const int v = getenv("TTS_HEAD_SCREEN_WAIT") ? atoi(getenv("TTS_HEAD_SCREEN_WAIT")) : 2;
+  return v == 1 || (v > 1 && rows >= v);
+}
+bool head_screen_check() {
+  static const bool v = getenv("TTS_HEAD_SCREEN_CHECK") && atoi(getenv("TTS_HEAD_SCREEN_CHECK"));
   return v;
 }
 
@@ -681,6 +726,10 @@ struct Ctx {
   // lm_head over B rows of `xin` + the pick (greedy argmax, or the sampling head) + finalize
   // (state update, next embedding -> w.x)
   void head_and_pick(const bf16_t* xin, int B, const StepState& st, const tts_gen_params& gp) {
+    if (!gp.do_sample && M.head_grid && head_screen_supported(B, c.hidden_size, c.vocab_size)) {
+      screened_head(xin, B, st, gp);
+      return;
+    }
     WgemmArgs ex;
     ex.seen = st.seen; ex.seen_stride = st.seen_stride; ex.penalty = gp.repetition_penalty;
     ex.eos_mask = st.eos_mask;
@@ -705,6 +754,42 @@ struct Ctx {
     }
     launch_finalize_greedy(ex.part_val, ex.part_idx, LOGITS_MAX_PARTS, nparts, st, B,
                            M.embed_rows.as<bf16_t>(), w.x.as<bf16_t>(), c.hidden_size, s);
+  }
+
+  // greedy pick through the int8 screen + exact recheck (lm_head_screen.hip): the same ids as
+  // the full lm_head launch above
+  void screened_head(const bf16_t* xin, int B, const StepState& st, const tts_gen_params& gp) {
+    const int rg = screened_head_parts(xin, B, st, gp);
+    launch_finalize_greedy(w.lpart_v.as<float>(), w.lpart_i.as<int>(), LOGITS_MAX_PARTS, rg, st, B,
+                           M.embed_rows.as<bf16_t>(), w.x.as<bf16_t>(), c.hidden_size, s);
+  }
+  // the screened head's launch (int8 screen + exact recompute of the units that can hold the
+  // argmax); returns the number of argmax partials per row
+  int screened_head_parts(const bf16_t* xin, int B, const StepState& st, const tts_gen_params& gp) {
+    const int HID = c.hidden_size, V = c.vocab_size;
+    HeadScreenArgs a;
+    a.M = B; a.K = HID; a.ldx = HID; a.V = V;
+    if (pending_norm == M.final_norm && xin == w.x.as<bf16_t>()) {
+      a.x = w.xn.as<bf16_t>();  // (a residual combine wrote RMSNorm(x, final norm))
+    } else {
+      a.x = xin; a.normw = M.final_norm; a.eps = c.rms_norm_eps;
+    }
+    a.q = M.head_q.as<int8_t>(); a.cst = M.head_c.as<float4>();
+    a.ur = M.head_grid * head_screen_waves();
+    a.w = M.lm_head;
+    const StreamPlan sp = stream_plan(V, HID, 1, e->num_cu);
+    a.hku = sp.ku; a.hur = sp.ur(); a.hKT = HID / 32; a.hkc = sp.kc;
+    a.seen = st.seen; a.seen_stride = st.seen_stride; a.penalty = gp.repetition_penalty;
+    a.eos_mask = st.eos_mask; a.counts = st.counts; a.freq_penalty = gp.frequency_penalty;
+    a.epoch = st.epoch; a.lbg = w.hlb.as<unsigned long long>();
+    a.arrive = (uint32_t*)(w.hlb.as<unsigned long long>() + 16 * 8);
+    a.spins = head_screen_wait(B) ? (1 << 14) : 0;
+    a.part_val = w.lpart_v.as<float>(); a.part_idx = w.lpart_i.as<int>(); a.part_stride = LOGITS_MAX_PARTS;
+    if (head_screen_check()) {
+      a.check = 1; a.ub = w.hub.as<float>(); a.ldu = V; a.err = w.ferr.as<int>() + 1;
+    }
+    launch_head_screen(a, M.head_grid, s);
+    return M.head_grid;
   }
 };
 
@@ -928,13 +1013,14 @@ int lm_gen_continue(Engine* e, int n_steps) {
 // the next read (the flag is cleared for the next generation).
 static void check_fattn(Engine* e, hipStream_t s) {
   if (!e->w.ferr.p) return;
-  int err = 0;
-  HIP_CHECK(hipMemcpyAsync(&err, e->w.ferr.p, 4, hipMemcpyDeviceToHost, s));
+  int err[2] = {0, 0};
+  HIP_CHECK(hipMemcpyAsync(err, e->w.ferr.p, 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  if (err) {
-    HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 4, s));
+  if (err[0] || err[1]) {
+    HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 8, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    TTS_REQUIRE(false, "fused QKV+attention: a granule wait timed out (results invalid)");
+    TTS_REQUIRE(!err[0], "fused QKV+attention: a granule wait timed out (results invalid)");
+    TTS_REQUIRE(false, "screened lm_head: an exact score above its int8 bound (TTS_HEAD_SCREEN_CHECK)");
   }
 }
 
@@ -1138,8 +1224,12 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
   TTS_REQUIRE(e->lm.loaded, "tts_lm_load has not been called");
   TTS_REQUIRE(rows >= 1 && rows <= e->w.cap_batch, "rows out of range");
   TTS_REQUIRE(ctx >= 1 && ctx <= e->lm.cfg.max_seq_len, "ctx out of range");
-  TTS_REQUIRE(which >= 0 && which <= 7 && iters >= 1, "bad kernel selector");
-  TTS_REQUIRE(which < 6 || Ctx(e, e->stream).fused_attn_ok(rows, true), "fused QKV+attention does not apply to this shape");
+  TTS_REQUIRE(which >= 0 && which <= 9 && iters >= 1, "bad kernel selector");
+  TTS_REQUIRE(which < 6 || which > 7 || Ctx(e, e->stream).fused_attn_ok(rows, true),
+              "fused QKV+attention does not apply to this shape");
+  TTS_REQUIRE(which < 8 || (e->lm.head_grid && rows <= 32 && head_screen_supported(rows, e->lm.cfg.hidden_size,
+                                                                                      e->lm.cfg.vocab_size)),
+              "the screened lm_head does not apply to this shape (or is off)");
   TTS_REQUIRE(which != 7 || (rows == 1 ? Ctx(e, e->stream).fused_oproj_ok() : Ctx(e, e->stream).fused_oproj_rows_ok(rows)),
               "fused o_proj does not apply to this shape (or is off)");
   hipStream_t s = e->stream;
@@ -1217,6 +1307,18 @@ void lm_bench_kernel(Engine* e, int which, int rows, int ctx, int iters, float* 
         b = 2.0 * QKV * HID + act_rw * (HID + QKV) + 2.0 * HID +
             (double)rows * c.num_kv_heads * ctx * c.head_dim * 2 * 2;
         if (which == 7) b += 2.0 * HID * HD + act_rw * (HD + 2 * HID);
+        break;
+      }
+      case 8:    // the greedy head's int8 screen + exact recheck (lm_head_screen.hip)
+      case 9: {  // the screen alone
+        tts_gen_params gp{};
+        gp.repetition_penalty = 1.1f;
+        X.pending_norm = nullptr;
+        X.screened_head_parts(e->w.x.as<bf16_t>(), rows, st, gp);
+        if (which == 8) launch_bump_epoch(st.epoch, s);  // (the step counter finalize advances)
+        // int8 matrix + per-column constants + rows + penalty bits (+ the recomputed units' bf16 tiles,
+        // a few dozen of 64 KiB, not counted)
+        b = (double)V * HID + 16.0 * V + act_rw * HID + rows * (V / 8.0);
         break;
       }
     }
@@ -1374,6 +1476,11 @@ std::string lm_step_plan(const tts_lm_config& c, int rows, int num_cu) {
   }
   e.lm.final_norm = next();
   e.lm.lm_head = next();
+  {
+    const StreamPlan hp = stream_plan(c.vocab_size, c.hidden_size, 1, num_cu);
+    if (head_screen_enabled() && head_screen_supported(1, c.hidden_size, c.vocab_size) && hp.ng == 1 && hp.ksplit == 1)
+      e.lm.head_grid = num_cu;
+  }
   e.w.cap_batch = e.lm.cfg.max_batch;
   e.w.kpart.bytes = kpart_bytes(c);  // (the size the plan checks; never dereferenced)
   std::vector<std::string> rec;

@@ -212,6 +212,42 @@ void launch_wgemm(const WgemmArgs& a, const WgemmPlan& p, int epi, bool norm, hi
 // workgroups (grid.y): fp32 partials [4][M][ldo] to a.part_out; a.K = K / 4 (lm_gemm_store.hip)
 void launch_wgemm_kslice(const WgemmArgs& a, int units, hipStream_t s);
 
+// ---- greedy lm_head as an exact two-pass argmax (lm_head_screen.hip): an int8 screen that
+// bounds every column's processed score, then (in the same launch) the units that can hold the
+// argmax recomputed exactly as the bf16 lm_head computes them
+struct HeadScreenArgs {
+  const bf16_t* x = nullptr;      // [M][ldx] rows (RMSNorm'ed here when normw)
+  int M = 0, K = 0, ldx = 0, V = 0;
+  const bf16_t* normw = nullptr;  // final RMSNorm weight, or nullptr (rows already normalised)
+  float eps = 0.f;
+  const int8_t* q = nullptr;      // int8 lm_head in the screen's block layout (launch_head_quant)
+  const float4* cst = nullptr;    // [V] {scale, |W - Wh|, |W|, |Wh|}
+  int ur = 0;                     // layout units per round = screen grid * head_screen_waves()
+  const bf16_t* w = nullptr;      // the tiled bf16 lm_head and its stream plan (ng 1, ksplit 1)
+  int hku = 8, hur = 0, hKT = 0, hkc = 1;
+  const uint32_t* seen = nullptr;
+  int seen_stride = 0;
+  float penalty = 1.f;
+  const int* eos_mask = nullptr;
+  const uint16_t* counts = nullptr;
+  float freq_penalty = 0.f;
+  const uint32_t* epoch = nullptr;      // the decode-step counter (finalize_greedy_kernel advances it)
+  unsigned long long* lbg = nullptr;    // [M][8 shards] maximum lower bound: (step << 32) | order key
+  uint32_t* arrive = nullptr;           // [8 shards, 64 B apart] workgroups that added their bounds (only grows)
+  int spins = 1 << 14;                  // polls (s_sleep 1 each) before the wait for them gives up (0: no wait)
+  float* part_val = nullptr;      // [M][part_stride] argmax partials, one per workgroup
+  int* part_idx = nullptr;
+  int part_stride = 0;
+  int check = 0;                  // 1: recompute every unit, check each score against its bound
+  float* ub = nullptr;            // check mode: [M][ldu] upper bound of every processed score
+  int ldu = 0;
+  int* err = nullptr;             // check mode: set to 1 when a score exceeds its bound
+};
+bool head_screen_supported(int M, int K, int V);
+int head_screen_waves();
+void launch_head_quant(const bf16_t* w, int V, int K, int ur, int8_t* q, float* cst, hipStream_t s);
+void launch_head_screen(const HeadScreenArgs& a, int grid, hipStream_t s);
+
 // ---- prefill GEMM (lm_pgemm.hip): many rows against the same tiled weights, LDS-staged
 // MFMA blocks; epilogues EPI_STORE / EPI_RESID / EPI_SWIGLU; no fused RMSNorm
 struct PgemmArgs {

@@ -373,7 +373,7 @@ class MI355XSpeechLM:
         ms, b = ctypes.c_float(), ctypes.c_double()
         # qkv_attn: QKV with the decode attention fused in (the one-row step's form);
         # qkv_attn_oproj: the same launch also carrying o_proj (the default 1..16-row step)
-        sel = {"qkv_attn": 6, "qkv_attn_oproj": 7}.get(which)
+        sel = {"qkv_attn": 6, "qkv_attn_oproj": 7, "head_screened": 8, "head_screen": 9}.get(which)
         sel = self.KERNELS.index(which) if sel is None else sel
         _lib.check(self._lib.tts_lm_bench_kernel(self._h, sel, rows, ctx, iters,
                                                  ctypes.byref(ms), ctypes.byref(b)))
