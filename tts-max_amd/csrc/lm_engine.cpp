@@ -788,6 +788,9 @@ struct Ctx {
     if (head_screen_check()) {
       a.check = 1; a.ub = w.hub.as<float>(); a.ldu = V; a.err = w.ferr.as<int>() + 1;
     }
+    static const int diag = getenv("TTS_HEAD_SCREEN_DIAG") ? atoi(getenv("TTS_HEAD_SCREEN_DIAG")) : 0;
+    a.diag = diag;
+    if (diag & 2) a.err = w.ferr.as<int>() + 1;  // (the count lands in ferr[3])
     launch_head_screen(a, M.head_grid, s);
     return M.head_grid;
   }
@@ -1013,9 +1016,13 @@ int lm_gen_continue(Engine* e, int n_steps) {
 // the next read (the flag is cleared for the next generation).
 static void check_fattn(Engine* e, hipStream_t s) {
   if (!e->w.ferr.p) return;
-  int err[2] = {0, 0};
-  HIP_CHECK(hipMemcpyAsync(err, e->w.ferr.p, 8, hipMemcpyDeviceToHost, s));
+  int err[4] = {0, 0, 0, 0};
+  HIP_CHECK(hipMemcpyAsync(err, e->w.ferr.p, 16, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  if (err[3]) {  // (TTS_HEAD_SCREEN_DIAG=2: units the screen recomputed since the last read)
+    fprintf(stderr, "head screen: %d units recomputed\n", err[3]);
+    HIP_CHECK(hipMemsetAsync((int*)e->w.ferr.p + 3, 0, 4, s));
+  }
   if (err[0] || err[1]) {
     HIP_CHECK(hipMemsetAsync(e->w.ferr.p, 0, 8, s));
     HIP_CHECK(hipStreamSynchronize(s));

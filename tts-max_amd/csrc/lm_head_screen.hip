@@ -411,7 +411,8 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
 
   // ---- exact recompute of the flagged units (one 16-row m-tile: M <= 16)
   constexpr int KT = K / 32, KTW = KT / kScrWaves;
-  const int nflag = *ntl;
+  const int nflag = (a.diag & 1) ? 0 : *ntl;  // (diag 1: timing probe without the recompute)
+  if ((a.diag & 2) && tid == 0) atomicAdd(a.err + 2, *ntl);  // (diag 2: count the flagged units)
   float bv[4];
   int bi[4];
 #pragma unroll

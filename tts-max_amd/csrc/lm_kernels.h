@@ -242,6 +242,7 @@ struct HeadScreenArgs {
   float* ub = nullptr;            // check mode: [M][ldu] upper bound of every processed score
   int ldu = 0;
   int* err = nullptr;             // check mode: set to 1 when a score exceeds its bound
+  int diag = 0;                   // probes only (TTS_HEAD_SCREEN_DIAG): 1 skip the recompute (wrong ids), 2 count flagged units
 };
 bool head_screen_supported(int M, int K, int V);
 int head_screen_waves();
