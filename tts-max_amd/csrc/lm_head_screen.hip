@@ -15,7 +15,8 @@
 //        |L_c - a_c| <= |L_c - x.W_c| + |x.(W_c - Wh_c)| + |(x - xh).Wh_c| + rounding of a_c
 //                    <= gam*|x|*|W_c| + |x|*r_c + |x - xh|*|Wh_c| + tiny   =: e_c
 //     (Cauchy-Schwarz; gam = 2*K*2^-24 bounds the fp32 accumulation of K bf16 products; r_c,
-//     |W_c|, |Wh_c| are computed in double at load and rounded up).  It writes ub_c =
+//     |W_c|, |Wh_c| are computed in double at load and rounded up; the fp32 roundings of a_c, e_c
+//     and the sums are covered by relative margins).  It writes ub_c =
 //     proc(bf16(a_c + e_c)) per (row, column) and the workgroup maximum of lb_c = proc(bf16(a_c
 //     - e_c)).  Every argmax c* of the exact scores has ub_{c*} >= s_{c*} >= max_c lb_c =: LB.
 //  2. head_recheck_kernel reduces LB, finds the 16-column tiles holding a column with ub >= LB
@@ -44,15 +45,10 @@ constexpr int kScrWaves = 4;  // screen workgroup: 4 waves, one per SIMD
 constexpr int kScrKU = 8;     // 1-KiB int8 blocks (64 k each) per stage
 constexpr int kScrR = 2;      // stages in flight per wave
 
-// up / down: the float nearest a double, rounded outward (bounds stay bounds)
+// the float nearest a double, rounded up (bounds stay bounds)
 TTS_DEV float f_up(double d) {
   float f = (float)d;
   if ((double)f < d) f = nextafterf(f, INFINITY);
-  return f;
-}
-TTS_DEV float f_down(double d) {
-  float f = (float)d;
-  if ((double)f > d) f = nextafterf(f, -INFINITY);
   return f;
 }
 TTS_DEV double wave_sum_f64(double v) {
@@ -269,7 +265,7 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
   }
   lds_barrier();  // (LDS only: the weight stream stays in flight)
 
-  const double gam = 2.0 * K / 16777216.0;
+  const float gam = 2.f * K / 16777216.f;
   float lbm[MT][2];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) lbm[mt][0] = lbm[mt][1] = -INFINITY;
@@ -319,13 +315,16 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
         const int m = 8 * mt + 2 * g4 + p;
         float ub = -INFINITY;
         if (m < M) {
-          const long long Si = (long long)acc[mt][2 * p] * 256 + acc[mt][2 * p + 1];
-          const double av = (double)Si * (double)rsx[m] * (double)cs.x;
-          const double e = (double)rnx[m] * ((double)cs.y + gam * (double)cs.z) + (double)rndx[m] * (double)cs.w +
-                           1e-12 * fabs(av) + 1e-30;
+          // fp32, every rounding covered: av is within 3 roundings (< 2^-22 |av|) of sx scale (X.q),
+          // e within 2^-22 of its value; the margins (2^-21 |av|, e (1 + 2^-20)) also cover the
+          // final sums' roundings, so ub / lb stay outside [L - true e, L + true e]
+          const float Sf = (float)((long long)acc[mt][2 * p] * 256 + acc[mt][2 * p + 1]);
+          const float av = Sf * rsx[m] * cs.x;
+          const float e = fmaf(rnx[m], fmaf(gam, cs.z, cs.y), rndx[m] * cs.w) * (1.f + 0x1p-20f) +
+                          fabsf(av) * 0x1p-21f + 1e-30f;
           const uint16_t* crow = a.counts ? a.counts + (size_t)m * a.seen_stride * 32 : nullptr;
-          ub = head_proc(rbf(f_up(av + e)), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eos[mt][p]);
-          const float lb = head_proc(rbf(f_down(av - e)), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eos[mt][p]);
+          ub = head_proc(rbf(av + e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eos[mt][p]);
+          const float lb = head_proc(rbf(av - e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eos[mt][p]);
           if (a.ub) a.ub[(size_t)m * a.ldu + c] = ub;  // (check mode)
           lbm[mt][p] = fmaxf(lbm[mt][p], lb);
         }
