@@ -309,8 +309,11 @@ def main():
                            prefill_roofline=prefill_roofline(arch, [len(q) for q in p32], a32))
         # the 32-row decode kernels: live HIP-event time, algorithmic bytes, PMC HBM traffic
         k32s = {}
-        for k in lm.KERNELS:  # (32 rows: the full lm_head; the screen takes <= 16)
-            ms, by = lm.bench_kernel(k, rows=32, ctx=ctx_mid, iters=args.kernel_iters)
+        for k in list(lm.KERNELS) + (["head_screened"] if screened else []):
+            try:
+                ms, by = lm.bench_kernel(k, rows=32, ctx=ctx_mid, iters=args.kernel_iters)
+            except Exception:  # noqa: BLE001 (the screen not on at 32 rows: the full lm_head)
+                continue
             k32s[k] = dict(avg_ms=round(ms, 5), bytes=round(by), gbs=round(by / ms / 1e6, 1), traffic=pmc(k, 32)[0])
         sec["bs32"]["kernels"] = k32s
         # configs[4]: streaming, bs=8, chunks of 25 codes voiced with 25 codes of left context

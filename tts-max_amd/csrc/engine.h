@@ -94,6 +94,7 @@ struct LmWork {
   DevBuf epoch;                                     // decode-step counter (u32; the hand-off's tags)
   DevBuf lpart_v, lpart_i;                          // lm_head argmax partials
   DevBuf hub, hlb;                                  // screened head: check-mode score bounds [B][V], per-row max lower bound (u64)
+  DevBuf hxq, hxs;                                  // screened head at 17..32 rows: the rows quantised [2B][hidden] i8, their stats
   DevBuf kpart;                                     // K-sliced GEMM fp32 partials [kc][rows][N]
   DevBuf ppart;                                     // prefill GEMM fp32 partials [chunks][rows][N] (lm_pgemm.hip)
   DevBuf slogits;                                   // sampling: processed fp32 logits [B][V]

@@ -297,11 +297,13 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   if (M.head_grid) {
-    w.hub.alloc((size_t)std::min(B, 16) * V * 4);
-    w.hlb.alloc(16 * 8 * 8 + 8 * 64);  // 16 rows x 8 shards of bounds + 8 arrival counters (64 B apart)
+    w.hub.alloc((size_t)std::min(B, 32) * V * 4);
+    w.hxq.alloc((size_t)2 * 32 * HID);
+    w.hxs.alloc((size_t)32 * 16);
+    w.hlb.alloc(32 * 8 * 8 + 8 * 64);  // 32 rows x 8 shards of bounds + 8 arrival counters (64 B apart)
     HIP_CHECK(hipMemsetAsync(w.hlb.p, 0, w.hlb.bytes, s));  // (below any step's key)
   } else {
-    w.hub.release(); w.hlb.release();
+    w.hub.release(); w.hlb.release(); w.hxq.release(); w.hxs.release();
   }
   w.row_slot.alloc((size_t)R * 4);
   w.row_pos.alloc((size_t)R * 4);
@@ -769,10 +771,18 @@ struct Ctx {
     const int HID = c.hidden_size, V = c.vocab_size;
     HeadScreenArgs a;
     a.M = B; a.K = HID; a.ldx = HID; a.V = V;
-    if (pending_norm == M.final_norm && xin == w.x.as<bf16_t>()) {
-      a.x = w.xn.as<bf16_t>();  // (a residual combine wrote RMSNorm(x, final norm))
+    const bool ready = pending_norm == M.final_norm && xin == w.x.as<bf16_t>();  // (a residual combine
+    if (ready) {                                                                 //  wrote RMSNorm(x, final norm))
+      a.x = w.xn.as<bf16_t>();
+    } else if (head_screen_prequant(B)) {
+      launch_rmsnorm(xin, HID, M.final_norm, c.rms_norm_eps, w.xn.as<bf16_t>(), HID, B, HID, s);
+      a.x = w.xn.as<bf16_t>();
     } else {
       a.x = xin; a.normw = M.final_norm; a.eps = c.rms_norm_eps;
+    }
+    if (head_screen_prequant(B)) {  // (17..32 rows: quantised once, not by every workgroup)
+      launch_head_rowquant(a.x, HID, B, HID, w.hxq.as<int8_t>(), w.hxs.as<float>(), s);
+      a.xq = w.hxq.as<int8_t>(); a.xstat = w.hxs.as<float>();
     }
     a.q = M.head_q.as<int8_t>(); a.cst = M.head_c.as<float4>();
     a.ur = M.head_grid * head_screen_waves();
@@ -782,7 +792,7 @@ struct Ctx {
     a.seen = st.seen; a.seen_stride = st.seen_stride; a.penalty = gp.repetition_penalty;
     a.eos_mask = st.eos_mask; a.counts = st.counts; a.freq_penalty = gp.frequency_penalty;
     a.epoch = st.epoch; a.lbg = w.hlb.as<unsigned long long>();
-    a.arrive = (uint32_t*)(w.hlb.as<unsigned long long>() + 16 * 8);
+    a.arrive = (uint32_t*)(w.hlb.as<unsigned long long>() + 32 * 8);
     a.spins = head_screen_wait(B) ? (1 << 14) : 0;
     a.part_val = w.lpart_v.as<float>(); a.part_idx = w.lpart_i.as<int>(); a.part_stride = LOGITS_MAX_PARTS;
     if (head_screen_check()) {

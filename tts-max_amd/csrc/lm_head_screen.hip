@@ -128,6 +128,47 @@ __global__ __launch_bounds__(256) void head_quant_kernel(const bf16_t* __restric
   }
 }
 
+// One normalised bf16 row (a wave, CPL 16-B chunks per lane, chunk j of lane l at k = 512 j + 8 l)
+// as the screen's integer row: X = rint(x / sx), sx = max|x| / 32639, stored as the int8 rows
+// hi (X = 256 hi + lo) and lo; nx >= |x|, ndx >= |x - sx X|.  (fp32 sums: their relative error,
+// < K 2^-24, and the sqrt's are covered by the 2^-10 margin; d = x - sx X is one fma, exact to
+// 2^-24 of itself; any X is valid: the bound uses the X taken)
+template <int CPL>
+TTS_DEV void quant_row(const u32x4_t (&v)[CPL], int lane, int8_t* hi_row, int8_t* lo_row, float& sx, float& nx,
+                       float& ndx) {
+  float mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fmaxf(fabsf(bf_lo(v[j][q])), fabsf(bf_hi(v[j][q]))));
+  mx = wave_max_dpp(mx);
+  sx = mx > 0.f ? mx / 32639.f : 1.f;
+  const float isx = 1.f / sx;
+  float s2 = 0.f, d2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    uint32_t hw[2] = {0u, 0u}, lw[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = (e & 1) ? bf_hi(v[j][e >> 1]) : bf_lo(v[j][e >> 1]);
+      const int X = max(-32639, min(32639, (int)rintf(x * isx)));
+      const float d = fmaf(-sx, (float)X, x);
+      s2 = fmaf(x, x, s2);
+      d2 = fmaf(d, d, d2);
+      const int hi = (X + 128) >> 8, lo = X - hi * 256;
+      hw[e >> 2] |= (uint32_t)(hi & 0xff) << (8 * (e & 3));
+      lw[e >> 2] |= (uint32_t)(lo & 0xff) << (8 * (e & 3));
+    }
+    const int k = j * 512 + lane * 8;
+    *(uint2*)(hi_row + k) = make_uint2(hw[0], hw[1]);
+    *(uint2*)(lo_row + k) = make_uint2(lw[0], lw[1]);
+  }
+  s2 = wave_sum_dpp(s2);
+  d2 = wave_sum_dpp(d2);
+  nx = sqrtf(s2) * (1.f + 0x1p-10f);
+  ndx = sqrtf(d2) * (1.f + 0x1p-10f) + 1e-30f;
+}
+
 // ------------------------------------------------------------------------- the screen ----
 // Workgroup = 4 waves; wave gw = blockIdx.x*4 + wave streams units gw, gw + ur, ... (ur = the
 // layout's units per round = grid * 4): KT8 / 8 stages of 8 KiB per unit, two stages in flight
@@ -155,15 +196,19 @@ TTS_DEV uint32_t f2key(float f) {
 }
 TTS_DEV float key2f(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k); }
 
-template <int MT, int KT8, int RPW>
+// PRE (17..32 rows): the rows come normalised (a.x) and quantised by head_rowquant_kernel (a.xq,
+// a.xstat: one pass instead of every workgroup quantising every row); the recompute then reads
+// its A fragments from a.x (L2) instead of an LDS copy, and the int8 image takes the LDS
+template <int MT, int KT8, int RPW, bool PRE>
 __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int K = KT8 * 64, ldA = K + 16, ldX = K + 8, KU = kScrKU, R = kScrR, S = KT8 / KU, CPL = K / 512;
   constexpr int MMAX = 8 * MT;  // rows of the int8 image (two A rows each)
+  constexpr int MTB = PRE ? 2 : 1;  // 16-row m-tiles of the exact recompute
   static_assert(S % R == 0, "stages per unit must be a multiple of the ring depth");
   int8_t* Al = (int8_t*)smem;                                       // [16 MT][ldA] int8
-  bf16_t* Xl = (bf16_t*)(smem + (size_t)16 * MT * ldA);             // [MMAX][ldX] normalised rows
-  float* rsx = (float*)(Xl + (size_t)MMAX * ldX);                   // [MMAX] sx
+  bf16_t* Xl = (bf16_t*)(smem + (size_t)16 * MT * ldA);             // [MMAX][ldX] normalised rows (!PRE)
+  float* rsx = (float*)(Xl + (PRE ? 0 : (size_t)MMAX * ldX));       // [MMAX] sx
   float* rnx = rsx + MMAX;                                          // [MMAX] |x| (rounded up)
   float* rndx = rnx + MMAX;                                         // [MMAX] |x - sx X|
   float* rlb = rndx + MMAX;                                         // [waves][MMAX] lower-bound maxima
@@ -171,22 +216,34 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
   float* umx = LBc + MMAX;                                          // [waves][kScrMaxUPW][MMAX] unit max of ub
   int* tl = (int*)(umx + kScrWaves * kScrMaxUPW * MMAX);            // [waves * kScrMaxUPW] flagged units
   int* ntl = tl + kScrWaves * kScrMaxUPW;
-  f32x4_t* xacc = (f32x4_t*)(ntl + 4);                              // [64] chain hand-off (16-B aligned)
+  f32x4_t* xacc = (f32x4_t*)(ntl + 4);                              // [MTB][64] chain hand-off (16-B aligned)
   const int M = a.M, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4, col = lane & 15;
 
   // ---- the rows (and the norm weight) first, then the weight stream
-  u32x4_t xv[RPW][CPL], gv[CPL];
+  constexpr int XQJ = PRE ? 2 * MMAX * K / 16 / (kScrWaves * 64) : 1;  // PRE: 16-B pieces of the image per thread
+  u32x4_t xv[PRE ? 1 : RPW][CPL], gv[CPL], xq[XQJ];
+  float st3[3] = {1.f, 0.f, 0.f};
+  if constexpr (PRE) {
 #pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const bf16_t* xr = a.x + (size_t)min(wave + 4 * r, M - 1) * a.ldx;
+    for (int j = 0; j < XQJ; ++j) {  // (rows past 2M: the last row again, never used)
+      const int c = tid + j * kScrWaves * 64, row = min(c / (K / 16), 2 * M - 1);
+      xq[j] = *(const u32x4_t*)(a.xq + (size_t)row * K + (c % (K / 16)) * 16);
+    }
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) xv[r][j] = *(const u32x4_t*)(xr + j * 512 + lane * 8);
+    for (int q = 0; q < 3; ++q) st3[q] = a.xstat[min(tid, M - 1) * 4 + q];
+  } else {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const bf16_t* xr = a.x + (size_t)min(wave + 4 * r, M - 1) * a.ldx;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) xv[r][j] = *(const u32x4_t*)(xr + j * 512 + lane * 8);
+    }
+    const bf16_t* nw = a.normw ? a.normw : a.x;  // (unconditional loads: exact vmcnt waits)
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) gv[j] = *(const u32x4_t*)(nw + j * 512 + lane * 8);
   }
-  const bf16_t* nw = a.normw ? a.normw : a.x;  // (unconditional loads: exact vmcnt waits)
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) gv[j] = *(const u32x4_t*)(nw + j * 512 + lane * 8);
 
   const int units = a.V >> 4, ur = a.ur;
   const int gw = blockIdx.x * kScrWaves + wave;
@@ -207,11 +264,19 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
   for (int j = 0; j < R; ++j) issue(wr[j]);
   __builtin_amdgcn_sched_barrier(0);
 
+  if constexpr (PRE) {
 #pragma unroll
-  for (int r = 0; r < RPW; ++r) {
+    for (int j = 0; j < XQJ; ++j) {
+      const int c = tid + j * kScrWaves * 64, row = c / (K / 16);
+      if (row < 2 * M) *(u32x4_t*)(Al + (size_t)row * ldA + (c % (K / 16)) * 16) = xq[j];
+    }
+    if (tid < M) { rsx[tid] = st3[0]; rnx[tid] = st3[1]; rndx[tid] = st3[2]; }
+  }
+#pragma unroll
+  for (int r = 0; r < (PRE ? 0 : RPW); ++r) {
     const int m = wave + 4 * r;
     if (m < M) {  // (wave-uniform)
-      u32x4_t* v = xv[r];
+      u32x4_t (&v)[CPL] = xv[r];
       if (a.normw) {
         float ss = 0.f;
 #pragma unroll
@@ -223,44 +288,11 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
           for (int q = 0; q < 4; ++q)
             v[j][q] = pack_bf2(bf_lo(gv[j][q]) * rbf(bf_lo(v[j][q]) * rr), bf_hi(gv[j][q]) * rbf(bf_hi(v[j][q]) * rr));
       }
-      float mx = 0.f;
 #pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        *(u32x4_t*)(Xl + (size_t)m * ldX + j * 512 + lane * 8) = v[j];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fmaxf(fabsf(bf_lo(v[j][q])), fabsf(bf_hi(v[j][q]))));
-      }
-      mx = wave_max_dpp(mx);
-      const float sx = mx > 0.f ? mx / 32639.f : 1.f, isx = 1.f / sx;
-      // (fp32 sums: their relative error, < K 2^-24, and the sqrt's are covered by the 2^-10
-      // margin below; d = x - sx X is one fma, exact to 2^-24 of itself; any X is valid: the
-      // bound uses the X taken)
-      float s2 = 0.f, d2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        uint32_t hw[2] = {0u, 0u}, lw[2] = {0u, 0u};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = (e & 1) ? bf_hi(v[j][e >> 1]) : bf_lo(v[j][e >> 1]);
-          const int X = max(-32639, min(32639, (int)rintf(x * isx)));
-          const float d = fmaf(-sx, (float)X, x);
-          s2 = fmaf(x, x, s2);
-          d2 = fmaf(d, d, d2);
-          const int hi = (X + 128) >> 8, lo = X - hi * 256;
-          hw[e >> 2] |= (uint32_t)(hi & 0xff) << (8 * (e & 3));
-          lw[e >> 2] |= (uint32_t)(lo & 0xff) << (8 * (e & 3));
-        }
-        const int k = j * 512 + lane * 8;
-        *(uint2*)(Al + (size_t)(2 * m) * ldA + k) = make_uint2(hw[0], hw[1]);
-        *(uint2*)(Al + (size_t)(2 * m + 1) * ldA + k) = make_uint2(lw[0], lw[1]);
-      }
-      s2 = wave_sum_dpp(s2);
-      d2 = wave_sum_dpp(d2);
-      if (lane == 0) {
-        rsx[m] = sx;
-        rnx[m] = sqrtf(s2) * (1.f + 0x1p-10f);
-        rndx[m] = sqrtf(d2) * (1.f + 0x1p-10f) + 1e-30f;
-      }
+      for (int j = 0; j < CPL; ++j) *(u32x4_t*)(Xl + (size_t)m * ldX + j * 512 + lane * 8) = v[j];
+      float sx, nx, ndx;
+      quant_row<CPL>(v, lane, Al + (size_t)(2 * m) * ldA, Al + (size_t)(2 * m + 1) * ldA, sx, nx, ndx);
+      if (lane == 0) { rsx[m] = sx; rnx[m] = nx; rndx[m] = ndx; }
     }
   }
   lds_barrier();  // (LDS only: the weight stream stays in flight)
@@ -408,14 +440,16 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
   }
   __syncthreads();
 
-  // ---- exact recompute of the flagged units (one 16-row m-tile: M <= 16)
+  // ---- exact recompute of the flagged units (MTB 16-row m-tiles)
   constexpr int KT = K / 32, KTW = KT / kScrWaves;
   const int nflag = (a.diag & 1) ? 0 : *ntl;  // (diag 1: timing probe without the recompute)
   if ((a.diag & 2) && tid == 0) atomicAdd(a.err + 2, *ntl);  // (diag 2: count the flagged units)
-  float bv[4];
-  int bi[4];
+  float bv[MTB][4];
+  int bi[MTB][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) { bv[r] = -INFINITY; bi[r] = 0x7fffffff; }
+  for (int mb = 0; mb < MTB; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { bv[mb][r] = -INFINITY; bi[mb][r] = 0x7fffffff; }
   // this wave's k-tiles of unit t (the lm_head layout: plan_tile(1, 1, hku, hur, units, KT, hkc))
   auto load = [&](u32x4_t (&wf)[KTW], int t) {
 #pragma unroll
@@ -428,40 +462,63 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
       wf[j] = __builtin_nontemporal_load((const u32x4_t*)a.w + (size_t)tile * 64 + lane);
     }
   };
+  // A fragments of this wave's k-tiles: the LDS rows, or (PRE) the normalised rows in global memory
+  // (the same for every unit: loaded once)
+  u32x4_t axg[PRE ? MTB : 1][PRE ? KTW : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int mb = 0; mb < MTB; ++mb)
+#pragma unroll
+      for (int j = 0; j < KTW; ++j)
+        axg[mb][j] = *(const u32x4_t*)(a.x + (size_t)min(16 * mb + col, M - 1) * a.ldx + (wave * KTW + j) * 32 + 8 * g4);
+  }
   const bf16_t* xrow = Xl + (size_t)min(col, M - 1) * ldX + 8 * g4;
   auto chain = [&](const u32x4_t (&wf)[KTW], int t) {
-    f32x4_t acc4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc4[MTB];
+#pragma unroll
+    for (int mb = 0; mb < MTB; ++mb) acc4[mb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kScrWaves; ++s) {
       if (wave == s) {
-        if (s > 0) acc4 = xacc[lane];
 #pragma unroll
-        for (int j = 0; j < KTW; ++j) {
-          const u32x4_t av = *(const u32x4_t*)(xrow + (s * KTW + j) * 32);
-          acc4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av),
-                                                         __builtin_bit_cast(bf16x8_t, wf[j]), acc4, 0, 0, 0);
+        for (int mb = 0; mb < MTB; ++mb)
+          if (s > 0) acc4[mb] = xacc[mb * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < KTW; ++j)
+#pragma unroll
+          for (int mb = 0; mb < MTB; ++mb) {
+            u32x4_t av;
+            if constexpr (PRE) av = axg[mb][j];
+            else av = *(const u32x4_t*)(xrow + (s * KTW + j) * 32);
+            acc4[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av),
+                                                               __builtin_bit_cast(bf16x8_t, wf[j]), acc4[mb], 0, 0, 0);
+          }
+        if (s < kScrWaves - 1) {
+#pragma unroll
+          for (int mb = 0; mb < MTB; ++mb) xacc[mb * 64 + lane] = acc4[mb];
         }
-        if (s < kScrWaves - 1) xacc[lane] = acc4;
       }
       lds_barrier();
     }
     if (wave == kScrWaves - 1) {
       const int n = t * 16 + col;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 4 * g4 + r;
-        if (m < M) {
-          const uint16_t* crow = a.counts ? a.counts + (size_t)m * a.seen_stride * 32 : nullptr;
-          const float v = head_proc(rbf(acc4[r]), a.seen[(size_t)m * a.seen_stride + (n >> 5)], n, a.penalty, crow,
-                                    a.freq_penalty, a.eos_mask[m]);
-          if (a.check && !(v <= a.ub[(size_t)m * a.ldu + n]) && v == v)
-            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v > bv[r] || (v == bv[r] && n < bi[r])) { bv[r] = v; bi[r] = n; }
+      for (int mb = 0; mb < MTB; ++mb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * mb + 4 * g4 + r;
+          if (m < M) {
+            const uint16_t* crow = a.counts ? a.counts + (size_t)m * a.seen_stride * 32 : nullptr;
+            const float v = head_proc(rbf(acc4[mb][r]), a.seen[(size_t)m * a.seen_stride + (n >> 5)], n, a.penalty,
+                                      crow, a.freq_penalty, a.eos_mask[m]);
+            if (a.check && !(v <= a.ub[(size_t)m * a.ldu + n]) && v == v)
+              __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v > bv[mb][r] || (v == bv[mb][r] && n < bi[mb][r])) { bv[mb][r] = v; bi[mb][r] = n; }
+          }
         }
-      }
     }
   };
-  if constexpr (KTW <= 16) {
+  if constexpr (KTW <= 16 && !PRE) {
     // two units in flight: the next flagged unit's tiles load while this one's chain runs (the
     // loads are unconditional — an index past the list repeats the last unit, never used — so
     // the chain's waits count only its own loads)
@@ -484,37 +541,60 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
   }
   if (wave == kScrWaves - 1) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int mb = 0; mb < MTB; ++mb)
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const float v2 = __shfl_xor(bv[r], o, 64);
-        const int i2 = __shfl_xor(bi[r], o, 64);
-        if (v2 > bv[r] || (v2 == bv[r] && i2 < bi[r])) { bv[r] = v2; bi[r] = i2; }
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float v2 = __shfl_xor(bv[mb][r], o, 64);
+          const int i2 = __shfl_xor(bi[mb][r], o, 64);
+          if (v2 > bv[mb][r] || (v2 == bv[mb][r] && i2 < bi[mb][r])) { bv[mb][r] = v2; bi[mb][r] = i2; }
+        }
+        const int m = 16 * mb + 4 * g4 + r;
+        if (col == 0 && m < M) {
+          a.part_val[(size_t)m * a.part_stride + blockIdx.x] = bv[mb][r];
+          a.part_idx[(size_t)m * a.part_stride + blockIdx.x] = bi[mb][r];
+        }
       }
-      const int m = 4 * g4 + r;
-      if (col == 0 && m < M) {
-        a.part_val[(size_t)m * a.part_stride + blockIdx.x] = bv[r];
-        a.part_idx[(size_t)m * a.part_stride + blockIdx.x] = bi[r];
-      }
-    }
   }
+}
+
+// One wave per row of normalised bf16 rows (17..32-row screen, PRE): X = rint(x / sx), sx =
+// max|x| / 32639, as the int8 rows 2m (hi) and 2m + 1 (lo) of xq [2M][K], and xstat[m] = {sx,
+// |x| (up), |x - sx X| (up), 0} — the screen prologue's arithmetic, once per row
+template <int CPL>
+__global__ __launch_bounds__(256) void head_rowquant_kernel(const bf16_t* __restrict__ x, int ldx, int M,
+                                                            int8_t* __restrict__ xq, float* __restrict__ xstat) {
+  constexpr int K = CPL * 512;
+  const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;  // (wave-uniform)
+  u32x4_t v[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) v[j] = *(const u32x4_t*)(x + (size_t)m * ldx + j * 512 + lane * 8);
+  float sx, nx, ndx;
+  quant_row<CPL>(v, lane, xq + (size_t)(2 * m) * K, xq + (size_t)(2 * m + 1) * K, sx, nx, ndx);
+  if (lane == 0) *(float4*)(xstat + m * 4) = make_float4(sx, nx, ndx, 0.f);
 }
 
 }  // namespace
 
-// rows the screen takes: one 16-row m-tile of the exact recompute, and the LDS of the int8 image
-// + the bf16 rows (K 2048: 16 rows; K 4096: 8)
-static int scr_mt(int M) { return M <= 8 ? 1 : 2; }
+// rows the screen takes: K 2048 up to 16 rows with the rows normalised and quantised in the
+// prologue (the int8 image + the bf16 rows share the LDS), 17..32 pre-quantised (PRE: the int8
+// image alone); K 4096 up to 8
+static int scr_mt(int M) { return M <= 8 ? 1 : (M <= 16 ? 2 : 4); }
 static size_t scr_lds(int M, int K) {
   const int mt = scr_mt(M), mm = 8 * mt;
-  return (size_t)16 * mt * (K + 16) + (size_t)mm * (K + 8) * 2 +
-         4 * ((size_t)mm * (4 + kScrWaves) + (size_t)kScrWaves * kScrMaxUPW * mm + kScrWaves * kScrMaxUPW + 4) + 64 * 16 + 16;
+  const bool pre = M > 16;
+  return (size_t)16 * mt * (K + 16) + (pre ? 0 : (size_t)mm * (K + 8) * 2) +
+         4 * ((size_t)mm * (4 + kScrWaves) + (size_t)kScrWaves * kScrMaxUPW * mm + kScrWaves * kScrMaxUPW + 4) +
+         2 * 64 * 16 + 16;
 }
 
 bool head_screen_supported(int M, int K, int V) {
-  return M >= 1 && M <= 16 && (K == 2048 || K == 4096) && V % 16 == 0 && V >= 4096 &&
+  return M >= 1 && M <= (K == 2048 ? 32 : 16) && (K == 2048 || K == 4096) && V % 16 == 0 && V >= 4096 &&
          (long long)V * K <= (long long)kWgemmMaxBytes && scr_lds(M, K) <= 160 * 1024;
 }
+bool head_screen_prequant(int M) { return M > 16; }
 int head_screen_waves() { return kScrWaves; }
 
 void launch_head_quant(const bf16_t* w, int V, int K, int ur, int8_t* q, float* cst, hipStream_t s) {
@@ -522,22 +602,34 @@ void launch_head_quant(const bf16_t* w, int V, int K, int ur, int8_t* q, float* 
   hipLaunchKernelGGL(head_quant_kernel, dim3((V + 3) / 4), dim3(256), 0, s, w, V, K, ur, q, (float4*)cst);
 }
 
+void launch_head_rowquant(const bf16_t* x, int ldx, int M, int K, int8_t* xq, float* xstat, hipStream_t s) {
+  if (K != 2048) throw std::runtime_error("head row quantiser: K 2048 only");
+  if (dry_record("head_rowquant_kernel")) return;
+  hipLaunchKernelGGL((head_rowquant_kernel<4>), dim3((M + 3) / 4), dim3(256), 0, s, x, ldx, M, xq, xstat);
+}
+
 void launch_head_screen(const HeadScreenArgs& a, int grid, hipStream_t s) {
+  const bool pre = head_screen_prequant(a.M);
   if (!head_screen_supported(a.M, a.K, a.V) || a.ur != grid * kScrWaves || (a.V / 16) > kScrMaxUPW * a.ur ||
-      a.hKT != a.K / 32 || grid > LOGITS_MAX_PARTS || !a.epoch || !a.lbg || !a.arrive || (a.check && !(a.ub && a.err)))
+      a.hKT != a.K / 32 || grid > LOGITS_MAX_PARTS || (pre && (a.K != 2048 || a.normw)))
     throw std::runtime_error("head screen: unsupported shape");
   const int mt = scr_mt(a.M), rpw = (a.M + kScrWaves - 1) / kScrWaves;
-  const int rp = rpw <= 1 ? 1 : (rpw <= 2 ? 2 : 4);
+  const int rp = pre ? 1 : (rpw <= 1 ? 1 : (rpw <= 2 ? 2 : 4));
   if (dry_record("head_screen_kernel<" + std::to_string(mt) + ", " + std::to_string(a.K / 64) + ", " +
-                 std::to_string(rp) + ">"))
+                 std::to_string(rp) + ", " + (pre ? "true" : "false") + ">"))
     return;
+  if (!a.epoch || !a.lbg || !a.arrive || (a.check && !(a.ub && a.err)) || (pre && !(a.xq && a.xstat)))
+    throw std::runtime_error("head screen: missing workspace");
   const size_t lds = scr_lds(a.M, a.K);
-#define TTS_SCR(MT_, KT8_, RP_) \
-  hipLaunchKernelGGL((head_screen_kernel<MT_, KT8_, RP_>), dim3(grid), dim3(kScrWaves * 64), lds, s, a)
+#define TTS_SCR(MT_, KT8_, RP_, PRE_) \
+  hipLaunchKernelGGL((head_screen_kernel<MT_, KT8_, RP_, PRE_>), dim3(grid), dim3(kScrWaves * 64), lds, s, a)
   if (a.K == 2048) {
-    if (rp == 1) TTS_SCR(1, 32, 1); else if (rp == 2) TTS_SCR(1, 32, 2); else TTS_SCR(2, 32, 4);
+    if (pre) TTS_SCR(4, 32, 1, true);
+    else if (rp == 1) TTS_SCR(1, 32, 1, false);
+    else if (rp == 2) TTS_SCR(1, 32, 2, false);
+    else TTS_SCR(2, 32, 4, false);
   } else {
-    if (rp == 1) TTS_SCR(1, 64, 1); else TTS_SCR(1, 64, 2);
+    if (rp == 1) TTS_SCR(1, 64, 1, false); else if (rp == 2) TTS_SCR(1, 64, 2, false); else TTS_SCR(2, 64, 4, false);
   }
 #undef TTS_SCR
 }

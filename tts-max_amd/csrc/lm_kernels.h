@@ -220,6 +220,8 @@ struct HeadScreenArgs {
   int M = 0, K = 0, ldx = 0, V = 0;
   const bf16_t* normw = nullptr;  // final RMSNorm weight, or nullptr (rows already normalised)
   float eps = 0.f;
+  const int8_t* xq = nullptr;     // (17..32 rows) the rows pre-quantised [2M][K] (launch_head_rowquant)
+  const float* xstat = nullptr;   //   and their {sx, |x|, |x - sx X|, 0} [M][4]
   const int8_t* q = nullptr;      // int8 lm_head in the screen's block layout (launch_head_quant)
   const float4* cst = nullptr;    // [V] {scale, |W - Wh|, |W|, |Wh|}
   int ur = 0;                     // layout units per round = screen grid * head_screen_waves()
@@ -245,7 +247,9 @@ struct HeadScreenArgs {
   int diag = 0;                   // probes only (TTS_HEAD_SCREEN_DIAG): 1 skip the recompute (wrong ids), 2 count flagged units
 };
 bool head_screen_supported(int M, int K, int V);
+bool head_screen_prequant(int M);  // rows quantised by launch_head_rowquant first (17..32 rows, K 2048)
 int head_screen_waves();
+void launch_head_rowquant(const bf16_t* x, int ldx, int M, int K, int8_t* xq, float* xstat, hipStream_t s);
 void launch_head_quant(const bf16_t* w, int V, int K, int ur, int8_t* q, float* cst, hipStream_t s);
 void launch_head_screen(const HeadScreenArgs& a, int grid, hipStream_t s);
 
