@@ -20,7 +20,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             name = r.get("Kernel_Name", "")
             vals.setdefault(name, []).append(float(r["Counter_Value"]))
     # the probed kernel = the wgemm/attention instantiation with the most dispatches
-    probed = {k: v for k, v in vals.items() if re.search(r"wgemm_kernel|attn_decode|attn_kernel", k)}
+    probed = {k: v for k, v in vals.items() if re.search(r"wgemm_kernel|attn_decode|attn_kernel|head_screen_kernel", k)}
     name, v = max(probed.items(), key=lambda kv: len(kv[1]))
     v = v[1:] if len(v) > 2 else v  # drop the warm-up launch
     kb = sum(v) / len(v)

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 fatal() { if [ $1 -ne 0 ]; then echo "stop: rc=$1 in $2"; exit $1; fi; }
 timeout -k 10 900 python -u -m pytest tests/test_gpu_head_screen.py tests/test_gpu_switches.py -k "head or HEAD" -v -rf --timeout 400 --timeout-method thread > $O/${T}_tests.log 2>&1; rc=$?
 tail -12 $O/${T}_tests.log; fatal $rc tests
-for r in 32 24; do
+for r in 32 8 1; do
   timeout -k 10 600 python -u scripts/env_ab_probe.py TTS_HEAD_SCREEN $r 2 > $O/${T}_ab_head_screen_$r.txt 2>&1; rc=$?
   cat $O/${T}_ab_head_screen_$r.txt; fatal $rc ab$r
 done

@@ -57,6 +57,14 @@ TTS_DEV double wave_sum_f64(double v) {
   return v;
 }
 
+// the maximum over the 16 lanes of each DPP row, in every lane (row_ror 1, 2, 4, 8: VALU speed)
+TTS_DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_mov<0x121>(v, v));
+  v = fmaxf(v, dpp_mov<0x122>(v, v));
+  v = fmaxf(v, dpp_mov<0x124>(v, v));
+  return fmaxf(v, dpp_mov<0x128>(v, v));
+}
+
 // The lm_head epilogue's processing of one bf16-rounded logit (lm_gemm_kernel.h EPI_LOGITS):
 // repetition penalty on seen ids, frequency penalty, min-new EOS mask.  Monotone in v.
 TTS_DEV float head_proc(float v, uint32_t seen_word, int n, float penalty, const uint16_t* counts_row,
@@ -189,6 +197,11 @@ TTS_DEV void quant_row(const u32x4_t (&v)[CPL], int lane, int8_t* hi_row, int8_t
 // continues wave w - 1's accumulator through LDS), the same epilogue — and the workgroup writes
 // its argmax partial (lowest index on ties) for finalize_greedy_kernel.
 constexpr int kScrMaxUPW = 16;  // units a wave streams (host-checked: units <= 16 * ur)
+#ifdef TTS_SCR_PROBE
+constexpr int kScrProbe = TTS_SCR_PROBE;  // timing probes only (scripts: wrong ids): 1 no MFMA, 2 no epilogue
+#else
+constexpr int kScrProbe = 0;
+#endif
 
 TTS_DEV uint32_t f2key(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -244,6 +257,12 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
 #pragma unroll
     for (int j = 0; j < CPL; ++j) gv[j] = *(const u32x4_t*)(nw + j * 512 + lane * 8);
   }
+
+  int eosr[MT][2];  // the rows' EOS masks (every unit's epilogue)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) eosr[mt][p] = a.eos_mask[min(8 * mt + 2 * g4 + p, M - 1)];
 
   const int units = a.V >> 4, ur = a.ur;
   const int gw = blockIdx.x * kScrWaves + wave;
@@ -311,15 +330,10 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
     const int c = u * 16 + col;
     const float4 cs = a.cst[c];
     uint32_t sw[MT][2];
-    int eos[MT][2];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int m = min(8 * mt + 2 * g4 + p, M - 1);
-        sw[mt][p] = a.seen[(size_t)m * a.seen_stride + (c >> 5)];
-        eos[mt][p] = a.eos_mask[m];
-      }
+      for (int p = 0; p < 2; ++p) sw[mt][p] = a.seen[(size_t)min(8 * mt + 2 * g4 + p, M - 1) * a.seen_stride + (c >> 5)];
     i32x4_t acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = i32x4_t{0, 0, 0, 0};
@@ -332,8 +346,12 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
           const int kb = (st + j) * KU + kk;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
-            const i32x4_t af = *(const i32x4_t*)(Al + aoff + (16 * mt + col) * ldA + kb * 64 + 16 * g4);
-            acc[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, __builtin_bit_cast(i32x4_t, wr[j][kk]), acc[mt], 0, 0, 0);
+            if constexpr (kScrProbe & 1) {  // (probe build: no A reads, no MFMA)
+              acc[mt][0] ^= (int)wr[j][kk][0];
+            } else {
+              const i32x4_t af = *(const i32x4_t*)(Al + aoff + (16 * mt + col) * ldA + kb * 64 + 16 * g4);
+              acc[mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, __builtin_bit_cast(i32x4_t, wr[j][kk]), acc[mt], 0, 0, 0);
+            }
           }
         }
         issue(wr[j]);
@@ -346,23 +364,29 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
       for (int p = 0; p < 2; ++p) {
         const int m = 8 * mt + 2 * g4 + p;
         float ub = -INFINITY;
+        if (kScrProbe & 2) {  // (probe build: no per-unit epilogue)
+          if (acc[mt][0] == 12345) a.part_val[0] = 0.f;
+          continue;
+        }
         if (m < M) {
           // fp32, every rounding covered: av is within 3 roundings (< 2^-22 |av|) of sx scale (X.q),
           // e within 2^-22 of its value; the margins (2^-21 |av|, e (1 + 2^-20)) also cover the
           // final sums' roundings, so ub / lb stay outside [L - true e, L + true e]
-          const float Sf = (float)((long long)acc[mt][2 * p] * 256 + acc[mt][2 * p + 1]);
+          // (X.q = 256 hi.q + lo.q; the two int -> fp32 conversions and the fma round to within
+          // 2^-23 (256 |hi.q| + |lo.q|), a term of its own: they may cancel)
+          const float hq = (float)acc[mt][2 * p], lq = (float)acc[mt][2 * p + 1];
+          const float Sf = fmaf(hq, 256.f, lq);
           const float av = Sf * rsx[m] * cs.x;
           const float e = fmaf(rnx[m], fmaf(gam, cs.z, cs.y), rndx[m] * cs.w) * (1.f + 0x1p-20f) +
-                          fabsf(av) * 0x1p-21f + 1e-30f;
+                          (fabsf(av) + fmaf(fabsf(hq), 256.f, fabsf(lq)) * rsx[m] * cs.x) * 0x1p-21f + 1e-30f;
           const uint16_t* crow = a.counts ? a.counts + (size_t)m * a.seen_stride * 32 : nullptr;
-          ub = head_proc(rbf(av + e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eos[mt][p]);
-          const float lb = head_proc(rbf(av - e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eos[mt][p]);
+          ub = head_proc(rbf(av + e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eosr[mt][p]);
+          const float lb = head_proc(rbf(av - e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eosr[mt][p]);
           if (a.ub) a.ub[(size_t)m * a.ldu + c] = ub;  // (check mode)
           lbm[mt][p] = fmaxf(lbm[mt][p], lb);
         }
         // the unit's maximum of ub per row (its 16 columns = the 16 lanes of the group)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) ub = fmaxf(ub, __shfl_xor(ub, o, 64));
+        ub = row16_max(ub);
         if (col == 0 && nu < kScrMaxUPW) umx[(wave * kScrMaxUPW + nu) * MMAX + m] = ub;
       }
   }
