@@ -97,11 +97,13 @@ def test_step_plan_lists_the_bench_launches():
     from tts_amd.speechlm import step_plan
 
     one = step_plan(configs.LM_ARCHS["tts1"], 1)
-    assert one[-2:] == ["head_screen_kernel<1, 32, 1>", "finalize_greedy_kernel"], one
+    assert one[-2:] == ["head_screen_kernel<1, 32, 1, false>", "finalize_greedy_kernel"], one
     assert len([k for k in one if k.startswith("wgemm_kernel<")]) == 3, one
     assert "attn_decode_kernel<64>" not in one  # (fused into the QKV launch)
     b32 = step_plan(configs.LM_ARCHS["tts1"], 32)
     assert "attn_decode_kernel<64>" in b32 and "splitk_combine_norm" in b32, b32
+    # 17..32 rows: the rows quantised once, then the screen with the int8 image alone in LDS
+    assert b32[-3:] == ["head_rowquant_kernel", "head_screen_kernel<4, 32, 1, true>", "finalize_greedy_kernel"], b32
     # 2..16 rows: the attention and o_proj ride the QKV launch (its FROWS instantiation), the
     # RMSNorms run in the consumers' prologues, no standalone norm pass
     b8 = step_plan(configs.LM_ARCHS["tts1"], 8)
