@@ -43,7 +43,10 @@ namespace {
 
 constexpr int kScrWaves = 4;  // screen workgroup: 4 waves, one per SIMD
 constexpr int kScrKU = 8;     // 1-KiB int8 blocks (64 k each) per stage
-constexpr int kScrR = 2;      // stages in flight per wave
+#ifndef TTS_SCR_R
+#define TTS_SCR_R 2
+#endif
+constexpr int kScrR = TTS_SCR_R;  // stages in flight per wave (experiment builds: -DTTS_SCR_R=4)
 
 // the float nearest a double, rounded up (bounds stay bounds)
 TTS_DEV float f_up(double d) {
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
     // (the A fragments are the same for every unit: one m-tile at K 2048 keeps them in registers
     // across units, 128 VGPRs; larger images are re-read from LDS per unit, not hoisted)
     int aoff = 0;
-    if constexpr (MT * KT8 > 32) asm volatile("" : "+v"(aoff));
+    if constexpr (MT * KT8 > 32 || kScrR > 2) asm volatile("" : "+v"(aoff));
     // this unit's epilogue operands, issued behind its first stages and ahead of their refills
     const int c = u * 16 + col;
     const float4 cs = a.cst[c];
