@@ -68,6 +68,26 @@ TTS_DEV float row16_max(float v) {
   return fmaxf(v, dpp_mov<0x128>(v, v));
 }
 
+// head_proc for the screen's bounds, without the division: the penalty as a product with the
+// reciprocal, then the result widened by 2^-21 of the magnitudes it came from (up for an upper
+// bound, down for a lower one) — it stays on its side of head_proc's exact value (every rounding
+// here is below 2^-22 of those magnitudes)
+template <bool UP>
+TTS_DEV float head_proc_bound(float v, uint32_t seen_word, int n, float penalty, float inv_penalty,
+                              const uint16_t* counts_row, float freq, int eos) {
+  const bool seen = (seen_word >> (n & 31)) & 1u;
+  float mag = fabsf(v);
+  if (seen) v = v * (v < 0.f ? penalty : inv_penalty);
+  mag = fmaxf(mag, fabsf(v));
+  if (counts_row) {
+    const float sub = freq * (float)counts_row[n];
+    v -= sub;
+    mag += fabsf(sub) + fabsf(v);
+  }
+  v = UP ? v + mag * 0x1p-21f : v - mag * 0x1p-21f;
+  return n == eos ? -INFINITY : v;
+}
+
 // The lm_head epilogue's processing of one bf16-rounded logit (lm_gemm_kernel.h EPI_LOGITS):
 // repetition penalty on seen ids, frequency penalty, min-new EOS mask.  Monotone in v.
 TTS_DEV float head_proc(float v, uint32_t seen_word, int n, float penalty, const uint16_t* counts_row,
@@ -319,7 +339,7 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
   }
   lds_barrier();  // (LDS only: the weight stream stays in flight)
 
-  const float gam = 2.f * K / 16777216.f;
+  const float gam = 2.f * K / 16777216.f, inv_pen = 1.f / a.penalty;
   float lbm[MT][2];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) lbm[mt][0] = lbm[mt][1] = -INFINITY;
@@ -383,8 +403,9 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
           const float e = fmaf(rnx[m], fmaf(gam, cs.z, cs.y), rndx[m] * cs.w) * (1.f + 0x1p-20f) +
                           (fabsf(av) + fmaf(fabsf(hq), 256.f, fabsf(lq)) * rsx[m] * cs.x) * 0x1p-21f + 1e-30f;
           const uint16_t* crow = a.counts ? a.counts + (size_t)m * a.seen_stride * 32 : nullptr;
-          ub = head_proc(rbf(av + e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eosr[mt][p]);
-          const float lb = head_proc(rbf(av - e), sw[mt][p], c, a.penalty, crow, a.freq_penalty, eosr[mt][p]);
+          ub = head_proc_bound<true>(rbf(av + e), sw[mt][p], c, a.penalty, inv_pen, crow, a.freq_penalty, eosr[mt][p]);
+          const float lb =
+              head_proc_bound<false>(rbf(av - e), sw[mt][p], c, a.penalty, inv_pen, crow, a.freq_penalty, eosr[mt][p]);
           if (a.ub) a.ub[(size_t)m * a.ldu + c] = ub;  // (check mode)
           lbm[mt][p] = fmaxf(lbm[mt][p], lb);
         }
@@ -648,8 +669,10 @@ void launch_head_screen(const HeadScreenArgs& a, int grid, hipStream_t s) {
   if (!a.epoch || !a.lbg || !a.arrive || (a.check && !(a.ub && a.err)) || (pre && !(a.xq && a.xstat)))
     throw std::runtime_error("head screen: missing workspace");
   const size_t lds = scr_lds(a.M, a.K);
+  HeadScreenArgs b = a;
+  if (grid % 8) b.spins = 0;  // (the wait's 8 arrival shards need equal shares of the grid)
 #define TTS_SCR(MT_, KT8_, RP_, PRE_) \
-  hipLaunchKernelGGL((head_screen_kernel<MT_, KT8_, RP_, PRE_>), dim3(grid), dim3(kScrWaves * 64), lds, s, a)
+  hipLaunchKernelGGL((head_screen_kernel<MT_, KT8_, RP_, PRE_>), dim3(grid), dim3(kScrWaves * 64), lds, s, b)
   if (a.K == 2048) {
     if (pre) TTS_SCR(4, 32, 1, true);
     else if (rp == 1) TTS_SCR(1, 32, 1, false);
