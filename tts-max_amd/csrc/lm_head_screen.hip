@@ -220,6 +220,10 @@ TTS_DEV void quant_row(const u32x4_t (&v)[CPL], int lane, int8_t* hi_row, int8_t
 // continues wave w - 1's accumulator through LDS), the same epilogue — and the workgroup writes
 // its argmax partial (lowest index on ties) for finalize_greedy_kernel.
 constexpr int kScrMaxUPW = 16;  // units a wave streams (host-checked: units <= 16 * ur)
+#ifndef TTS_SCR_DB32
+#define TTS_SCR_DB32 0
+#endif
+constexpr bool kScrDB32 = TTS_SCR_DB32;  // two flagged units in flight at K 4096 too (AGPRs hold the second): measured slower (165 -> 167 us at TTS-1-Max 8 rows), off
 #ifdef TTS_SCR_PROBE
 constexpr int kScrProbe = TTS_SCR_PROBE;  // timing probes only (scripts: wrong ids): 1 no MFMA, 2 no epilogue
 #else
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
         }
     }
   };
-  if constexpr (KTW <= 16 && !PRE) {
+  if constexpr (!PRE && (KTW <= 16 || kScrDB32)) {
     // two units in flight: the next flagged unit's tiles load while this one's chain runs (the
     // loads are unconditional — an index past the list repeats the last unit, never used — so
     // the chain's waits count only its own loads)
