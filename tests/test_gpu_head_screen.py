@@ -37,6 +37,12 @@ w = synth.lm_weights_device(arch, 0x5EED, torch.device("cuda", 0))
 if mode == "twins":
     t = w["model.embed_tokens.weight" if arch.tie_word_embeddings else "lm_head.weight"]
     t[1::2] = t[0::2]
+if mode == "outliers":  # heavy-tailed rows: every 7th row x8, one element in 64 of the matrix x40
+    t = w["model.embed_tokens.weight" if arch.tie_word_embeddings else "lm_head.weight"]
+    g = torch.Generator(device=t.device).manual_seed(5)
+    t[::7] *= 8
+    mask = torch.rand(t.shape, generator=g, device=t.device) < 1.0 / 64
+    t[mask] *= 40
 cases = [(1, 1.0), (1, 1.1), (8, 1.4), (24, 1.1), (32, 1.0)] if mode != "twins" else [(1, 1.0), (8, 1.0), (32, 1.0)]
 m = MI355XSpeechLM(arch, w, max_batch=32, max_seq_len=400, id_to_code=vocab.id_to_code())
 del w
@@ -78,6 +84,16 @@ def test_check_mode_finds_every_score_inside_its_bound():
     checked = _run("TTS_HEAD_SCREEN_CHECK=1", "tts1")
     full = _run("TTS_HEAD_SCREEN=0", "tts1")
     assert checked == full
+
+
+def test_heavy_tailed_weights_stay_inside_their_bounds():
+    """Outlier rows and elements (far from the uniform synthetic weights): the per-column scale
+    of the int8 copy gets coarse, the bounds wide — every exact score must still sit inside its
+    bound (check mode) and the pick must still be the full head's."""
+    checked = _run("TTS_HEAD_SCREEN_CHECK=1", "tts1", "outliers")
+    full = _run("TTS_HEAD_SCREEN=0", "tts1", "outliers")
+    screened = _run(None, "tts1", "outliers")
+    assert checked == full and screened == full
 
 
 def test_exact_ties_take_the_lowest_id():
