@@ -470,8 +470,8 @@ __global__ __launch_bounds__(kScrWaves * 64) void head_screen_kernel(HeadScreenA
     }
   }
   __syncthreads();
-  if (tid < M * 8) {
-    const int m = tid >> 3;
+  if (tid < M * 8) {  // (also without the wait: the other shards' maxima so far cut the recompute,
+    const int m = tid >> 3;  //  one row 75 -> 68 us, profiles/r6am_ab_shardread_1.txt)
     const unsigned long long cur = __hip_atomic_load(a.lbg + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float v = (cur >> 32) == ep ? key2f((uint32_t)cur) : -INFINITY;
 #pragma unroll
