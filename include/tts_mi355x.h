@@ -104,7 +104,10 @@ typedef struct {
  * Optional tensors "rope.cos" / "rope.sin" ([max_seq_len, head_dim], bf16) override the
  * engine-computed RoPE table (the Python host passes the table computed exactly as
  * LlamaRotaryEmbedding.forward does).  Optional "vocab.id_to_code" (int32 [vocab]) is the
- * token-id -> speech-code LUT (-1 for non-speech ids), see tts_lm_id_to_code. */
+ * token-id -> speech-code LUT (-1 for non-speech ids), see tts_lm_id_to_code.
+ * Greedy steps pick through an int8 copy of the lm_head made here (vocab x hidden bytes more
+ * device memory) — the same ids as the bf16 lm_head; TTS_HEAD_SCREEN=0 at load
+ * skips it. */
 tts_status tts_lm_load(tts_engine* e, const tts_lm_config* cfg, const tts_tensor_desc* t,
                        int32_t n);
 
