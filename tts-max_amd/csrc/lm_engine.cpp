@@ -24,11 +24,26 @@ static constexpr int kPollEvery = 8;
 static constexpr int kPrefillChunk = 64;   // rows per GEMM launch (MFMA A-tiles of 16)
 static constexpr int kMaxPrefillRows = 8192;
 
-// the greedy lm_head's int8 screen + exact recheck (lm_head_screen.hip); TTS_HEAD_SCREEN=0: off
+// The greedy lm_head as an exact two-pass argmax (lm_head_screen.hip): default on;
+// TTS_HEAD_SCREEN=0 streams the full bf16 lm_head for greedy steps too (the same ids)
 static bool head_screen_enabled() {
   static const bool v = !(getenv("TTS_HEAD_SCREEN") && !atoi(getenv("TTS_HEAD_SCREEN")));
   return v;
 }
+// ... whose workgroups wait for every workgroup's bounds before flagging their units (the
+// exact candidate set; TTS_HEAD_SCREEN_WAIT=0: never, 1: always, n > 1 (default 2): from n rows —
+// one row: 69 vs 73 us, 8 rows: 79 vs 96 us without, profiles/r6w_ab_head_wait_*).  Same bits
+// either way: a lower LB only flags more units
+static bool head_screen_wait(int rows) {
+  static const int v = getenv("TTS_HEAD_SCREEN_WAIT") ? atoi(getenv("TTS_HEAD_SCREEN_WAIT")) : 2;
+  return v == 1 || (v > 1 && rows >= v);
+}
+// TTS_HEAD_SCREEN_CHECK=1: every unit recomputed and each exact score checked against its bound
+static bool head_screen_check() {
+  static const bool v = getenv("TTS_HEAD_SCREEN_CHECK") && atoi(getenv("TTS_HEAD_SCREEN_CHECK"));
+  return v;
+}
+
 
 int64_t numel(const tts_tensor_desc& d) {
   int64_t n = 1;
@@ -297,7 +312,8 @@ void lm_load(Engine* e, const tts_lm_config* cfgp, const tts_tensor_desc* t, int
   w.lpart_v.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   w.lpart_i.alloc((size_t)B * LOGITS_MAX_PARTS * 4);
   if (M.head_grid) {
-    w.hub.alloc((size_t)std::min(B, 32) * V * 4);
+    if (head_screen_check()) w.hub.alloc((size_t)std::min(B, 32) * V * 4);  // (check mode's bounds)
+    else w.hub.release();
     w.hxq.alloc((size_t)2 * 32 * HID);
     w.hxs.alloc((size_t)32 * 16);
     w.hlb.alloc(32 * 8 * 8 + 8 * 64);  // 32 rows x 8 shards of bounds + 8 arrival counters (64 B apart)
@@ -376,22 +392,6 @@ bool use_fused_oproj_rows() {
 // canonical sum order: the same bits)
 bool norm_prologue32() {
   static const bool v = getenv("TTS_NORM_PROLOGUE32") && atoi(getenv("TTS_NORM_PROLOGUE32"));
-  return v;
-}
-
-// The greedy lm_head as an exact two-pass argmax (lm_head_screen.hip): default on;
-// TTS_HEAD_SCREEN=0 streams the full bf16 lm_head for greedy steps too (the same ids);
-// TTS_HEAD_SCREEN_CHECK=1 recomputes every tile and checks each score against its bound
-// ... whose workgroups wait for every workgroup's bounds before flagging their units (the
-// exact candidate set; TTS_HEAD_SCREEN_WAIT=0: never, 1: always, n > 1 (default 2): from n rows —
-// one row: 69 vs 73 us, 8 rows: 79 vs 96 us without, profiles/r6w_ab_head_wait_*).  Same bits
-// either way: a lower LB only flags more units
-bool head_screen_wait(int rows) {
-  static const int v = getenv("TTS_HEAD_SCREEN_WAIT") ? atoi(getenv("TTS_HEAD_SCREEN_WAIT")) : 2;
-  return v == 1 || (v > 1 && rows >= v);
-}
-bool head_screen_check() {
-  static const bool v = getenv("TTS_HEAD_SCREEN_CHECK") && atoi(getenv("TTS_HEAD_SCREEN_CHECK"));
   return v;
 }
 
